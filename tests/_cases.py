@@ -1,0 +1,96 @@
+"""Seeded test inputs shared by CPU and GPU tests (numpy only)."""
+
+from __future__ import annotations
+
+import numpy as np
+
+from trex_amd.topology import create_balanced_binary_tree, random_topologies
+
+
+def simulate_leaves(n_leaves, seq_len, n_states, n_mutations, seed):
+    """numpy restatement of trex's ground-truth simulation.
+
+    src/trex/ground_truth.py:20-52 (mutate: exactly n_mutations sites get a
+    random non-zero offset mod n_states) and :112-197 (root = zeros; node
+    numbering leaves 0..n-1, parent of 2i, 2i+1 is n+i).  JAX's PRNG stream is
+    not reproducible, so only the process is restated.  Returns
+    (all_sequences (n_all, L) int8, adjacency (n_all, n_all) float32).
+    """
+    rng = np.random.default_rng(seed)
+    n_anc = n_leaves - 1
+    n_all = n_leaves + n_anc
+    seqs = np.zeros((n_all, seq_len), dtype=np.int8)
+
+    def mutate(parent):
+        child = parent.copy()
+        if n_mutations > 0:
+            pos = rng.choice(seq_len, size=n_mutations, replace=False)
+            off = rng.integers(1, n_states, size=n_mutations)
+            child[pos] = (child[pos] + off) % n_states
+        return child
+
+    for i in range(n_anc):
+        parent_idx = n_all - 1 - i
+        p_i = parent_idx - n_leaves
+        seqs[2 * p_i] = mutate(seqs[parent_idx])
+        seqs[2 * p_i + 1] = mutate(seqs[parent_idx])
+    adj = np.zeros((n_all, n_all), dtype=np.float32)
+    for i in range(n_anc):
+        adj[2 * i, n_leaves + i] = 1
+        adj[2 * i + 1, n_leaves + i] = 1
+    return seqs, adj
+
+
+def hamming(n_states):
+    return (np.ones((n_states, n_states)) - np.eye(n_states)).astype(np.float32)
+
+
+def int_cost(n_states, seed, lo=1, hi=4):
+    rng = np.random.default_rng(seed)
+    c = rng.integers(lo, hi + 1, size=(n_states, n_states)).astype(np.float32)
+    c = np.triu(c, 1)
+    c = c + c.T
+    return c
+
+
+def random_leaves(B, n_leaves, L, n_states, seed, missing=0.0):
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, n_states, size=(B, n_leaves, L)).astype(np.int8)
+    if missing > 0:
+        m = rng.random((B, n_leaves, L)) < missing
+        x[m] = -1
+    return x
+
+
+def balanced_children(n_leaves, B=1):
+    from trex_amd.topology import children_from_adjacency
+
+    ch = children_from_adjacency(create_balanced_binary_tree(n_leaves))
+    return np.repeat(ch, B, axis=0)
+
+
+def weird_children(case):
+    """Balanced 8-leaf child lists exercising trex's quirks (sankoff.py:60,67).
+
+    "fwdref": node 8 lists internal node 10 (> 8) -> 1e5 row in the DP, but the
+              backtrack still visits 10 from 8 (last visit wins); node 9 has
+              a -1 fill (second child missing).
+    "dag":    node 9 is a child of both 12 and 13; node 10 is an orphan.
+    "cycle":  node 8 lists its ancestor 12 -> the reference backtrack never
+              terminates (forward DP is still defined).
+    """
+    ch = balanced_children(8)[0].copy()
+    if case == "fwdref":
+        ch[8] = (0, 10)
+        ch[9, 1] = -1
+    elif case == "dag":
+        ch[13] = (9, 11)
+    elif case == "cycle":
+        ch[8] = (0, 12)
+    else:
+        raise ValueError(case)
+    return ch
+
+
+__all__ = ["simulate_leaves", "hamming", "int_cost", "random_leaves", "balanced_children",
+           "weird_children", "random_topologies", "create_balanced_binary_tree"]

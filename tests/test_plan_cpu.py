@@ -1,0 +1,127 @@
+"""CPU tests of the host side of libtrexhip.so: exports, the topology planner
+(checked by executing its program with a numpy interpreter), adjacency
+conversion.  No kernel is launched here."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from _cases import balanced_children, int_cost, random_leaves, random_topologies, weird_children
+from oracle.sankoff_ref import SENTINEL, leaf_dp, trex_children_table
+from oracle.softmin_ref import batched_fwd_bwd_ref
+from trex_amd import TreePlan, children_from_adjacency, create_balanced_binary_tree, lib
+from trex_amd._lib import SIGNATURES
+from trex_amd.topology import adjacency_from_children
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    with open(os.path.join(ROOT, "include", "trex_hip.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(trex_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    handle = ctypes.CDLL(str(lib()._name))
+    names = _header_functions()
+    assert len(names) >= 9
+    for n in names:
+        assert hasattr(handle, n), n
+        assert n in SIGNATURES, f"{n} missing from trex_amd._lib.SIGNATURES"
+
+
+def test_children_from_adjacency_matches_trex_rule():
+    adj = create_balanced_binary_tree(16)
+    adj[-1, -1] = 1  # root self loop is removed by run_sankoff (sankoff.py:141)
+    ch = children_from_adjacency(adj)[0]
+    np.testing.assert_array_equal(ch, trex_children_table(adj))
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        a = (rng.random((9, 9)) < 0.3).astype(np.float32)
+        a[rng.random((9, 9)) < 0.1] = 0.5  # non-1 values are not edges (== 1 test)
+        np.testing.assert_array_equal(children_from_adjacency(a)[0], trex_children_table(a))
+
+
+def _interpret(plan: TreePlan, b, leaves, cost):
+    """Execute the encoded forward program with an explicit slot stack."""
+    steps = plan.fwd_steps[b]
+    Q = cost.shape[0]
+    L = leaves.shape[-1]
+    slots = {}
+    dp = np.full((plan.n_int, L, Q), np.nan)
+    lD = leaf_dp(leaves, Q)
+    last = None
+    for row_desc, da, db, flags in steps:
+        row = row_desc & 0xFFFF
+        oslot = (row_desc >> 16) & 0xFF
+        acc = np.zeros((L, Q))
+        for d in (da, db):
+            kind = (d >> 24) & 3
+            if kind == 1:
+                D = lD[d & 0xFFFF]
+            elif kind == 2:
+                s = (d >> 16) & 0xFF
+                D = slots[s]
+                assert np.array_equal(D, dp[d & 0xFFFF]), "slot clobbered"
+            else:
+                D = np.full((L, Q), SENTINEL)
+            acc = acc + (cost[None] + D[:, None, :]).min(axis=2)
+        dp[row] = acc
+        if oslot != 0xFF:
+            slots[oslot] = acc
+        last = row
+    assert last == plan.n_int - 1, "root must be the last step"
+    return dp
+
+
+@pytest.mark.parametrize("kind", ["random", "balanced", "fwdref", "dag", "cycle"])
+def test_plan_program_reproduces_oracle(kind):
+    if kind == "random":
+        ch = random_topologies(4, 40, seed=1)
+    elif kind == "balanced":
+        ch = balanced_children(64, B=2)
+    else:
+        ch = weird_children(kind)[None]
+    plan = TreePlan(ch)
+    n_all = ch.shape[1]
+    nl = (n_all + 1) // 2
+    leaves = random_leaves(ch.shape[0], nl, 11, 4, seed=2, missing=0.1)
+    cost = int_cost(4, seed=3)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, 0.0)
+    for b in range(ch.shape[0]):
+        dp = _interpret(plan, b, leaves[b], cost.astype(np.float64))
+        np.testing.assert_array_equal(dp.transpose(0, 2, 1), ref["dp"][b])
+    assert plan.backtrack_ok == (0 if kind == "cycle" else 1)
+
+
+def test_plan_slot_counts_are_sethi_ullman():
+    for n, want in [(8, 3), (64, 6), (256, 8)]:
+        assert TreePlan.from_adjacency(create_balanced_binary_tree(n)).n_slots == want
+    # a caterpillar needs a single slot
+    n = 20
+    ch = np.full((1, 2 * n - 1, 2), -1, np.int32)
+    ch[0, n] = (0, 1)
+    for k in range(1, n - 1):
+        ch[0, n + k] = (k + 1, n + k - 1)
+    assert TreePlan(ch).n_slots == 1
+
+
+def test_plan_rejects_bad_children():
+    from trex_amd import TrexError
+
+    ch = balanced_children(8)
+    ch[0, 9, 0] = 99
+    with pytest.raises(TrexError):
+        TreePlan(ch)
+
+
+def test_adjacency_roundtrip():
+    ch = random_topologies(3, 12, seed=5)
+    np.testing.assert_array_equal(children_from_adjacency(adjacency_from_children(ch)), ch)

@@ -1,0 +1,288 @@
+// Host-side topology planner for libtrexhip.so.
+//
+// Turns trex's per-node child lists (jnp.where(adj[:, node] == 1, size=2,
+// fill_value=-1), src/trex/sankoff.py:60) into a per-tree "program" the HIP
+// kernels execute with wave-uniform control flow:
+//
+//  * forward steps in a post-order that evaluates the child needing more
+//    stack slots first (Sethi-Ullman), so live internal DP vectors fit a
+//    log2(n)+1-deep per-lane LDS stack instead of being re-read from HBM;
+//  * the child rules of trex's run_dp: c == -1 or c >= node reads a row that
+//    still holds the 1e5 init (sankoff.py:60,67,152), c < n_leaves is a leaf,
+//    otherwise an already computed internal row;
+//  * adjoint flags for the reverse sweep (which reverse step first writes a
+//    child's cotangent slot, which nodes the root never reaches);
+//  * the reference backtrack's visiting order (sankoff.py:212-265), simulated
+//    once on the topology (the DFS node sequence does not depend on states),
+//    reduced to "node x takes its state from parent p at x's last visit".
+//
+// This is integer work on B * n_all entries, done once per topology (the
+// reference re-traces per static shape, sankoff.py:114).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <queue>
+#include <set>
+#include <vector>
+
+#include "trex_common.h"
+
+namespace trex {
+
+namespace {
+
+constexpr int kKindSent = 0, kKindLeaf = 1, kKindInt = 2;
+
+struct Child {
+  int kind;
+  int index;  // leaf index or internal row
+};
+
+// One tree.  Returns false on a malformed child id.
+bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
+                   int* n_slots, int* bt_ok, int* n_dag, int* n_unreached) {
+  const int nl = (n_all + 1) / 2;
+  const int ni = n_all - nl;
+  std::vector<Child> kids(2 * ni);
+  std::vector<int> refs(ni, 0);
+  for (int r = 0; r < ni; ++r) {
+    const int node = nl + r;
+    for (int k = 0; k < 2; ++k) {
+      const int c = ch[2 * node + k];
+      if (c < -1 || c >= n_all) return false;
+      Child cd;
+      if (c == -1 || c >= node) {
+        cd = {kKindSent, 0};
+      } else if (c < nl) {
+        cd = {kKindLeaf, c};
+      } else {
+        cd = {kKindInt, c - nl};
+        refs[c - nl] += 1;
+      }
+      kids[2 * r + k] = cd;
+    }
+  }
+  int dag = 0;
+  for (int r = 0; r < ni; ++r) dag += refs[r] > 1;
+  *n_dag = dag;
+
+  // Sethi-Ullman need, rows in increasing order (internal children are lower)
+  std::vector<int> need(ni, 1);
+  for (int r = 0; r < ni; ++r) {
+    int a = 0, b = 0;
+    for (int k = 0; k < 2; ++k) {
+      const Child& cd = kids[2 * r + k];
+      if (cd.kind == kKindInt) {
+        const int n = need[cd.index];
+        if (n > a) { b = a; a = n; } else if (n > b) { b = n; }
+      }
+    }
+    need[r] = std::max({1, a, b + 1});
+  }
+
+  // schedule: post-order DFS, heavier child first; orphans first, root last
+  std::vector<int> order;
+  order.reserve(ni);
+  std::vector<char> done(ni, 0);
+  auto visit = [&](int start) {
+    std::vector<std::pair<int, int>> st;  // (row, phase)
+    st.push_back({start, 0});
+    while (!st.empty()) {
+      auto [r, ph] = st.back();
+      st.pop_back();
+      if (done[r]) continue;
+      if (ph == 1) {
+        done[r] = 1;
+        order.push_back(r);
+        continue;
+      }
+      st.push_back({r, 1});
+      int c0 = -1, c1 = -1;
+      if (kids[2 * r].kind == kKindInt) c0 = kids[2 * r].index;
+      if (kids[2 * r + 1].kind == kKindInt) c1 = kids[2 * r + 1].index;
+      // push the lighter first so the heavier is evaluated first
+      int heavy = c0, light = c1;
+      if (c0 < 0 || (c1 >= 0 && need[c1] > need[c0])) { heavy = c1; light = c0; }
+      if (light >= 0 && !done[light]) st.push_back({light, 0});
+      if (heavy >= 0 && !done[heavy]) st.push_back({heavy, 0});
+    }
+  };
+  for (int r = 0; r < ni - 1; ++r)
+    if (refs[r] == 0) visit(r);
+  visit(ni - 1);
+  if ((int)order.size() != ni) return false;  // unreachable in a DAG of lower ids
+
+  // slot simulation
+  std::vector<int> remaining(refs), slot(ni, 0xFF);
+  std::set<int> free_slots;
+  int top = 0, maxs = 0;
+  for (int r : order) {
+    for (int k = 0; k < 2; ++k) {
+      const Child& cd = kids[2 * r + k];
+      if (cd.kind != kKindInt) continue;
+      if (--remaining[cd.index] == 0) free_slots.insert(slot[cd.index]);
+    }
+    if (refs[r] > 0) {
+      int s;
+      if (!free_slots.empty()) {
+        s = *free_slots.begin();
+        free_slots.erase(free_slots.begin());
+      } else {
+        s = top++;
+      }
+      slot[r] = s;
+      maxs = std::max(maxs, s + 1);
+    }
+  }
+  if (maxs > 250) return false;
+  *n_slots = maxs;
+
+  // reachability from the root along real internal edges (adjoint support)
+  std::vector<char> reach(ni, 0);
+  reach[ni - 1] = 1;
+  for (int r = ni - 1; r >= 0; --r) {
+    if (!reach[r]) continue;
+    for (int k = 0; k < 2; ++k)
+      if (kids[2 * r + k].kind == kKindInt) reach[kids[2 * r + k].index] = 1;
+  }
+  int unr = 0;
+  for (int r = 0; r < ni; ++r) unr += !reach[r];
+  *n_unreached = unr;
+
+  // encode forward steps; set/accumulate flags follow the reverse order
+  std::vector<char> seen(ni, 0);
+  std::vector<int32_t> enc(4 * ni);
+  for (int k = ni - 1; k >= 0; --k) {
+    const int r = order[k];
+    int32_t* e = &enc[4 * k];
+    e[0] = (r & 0xFFFF) | ((slot[r] & 0xFF) << 16);
+    for (int j = 0; j < 2; ++j) {
+      const Child& cd = kids[2 * r + j];
+      int32_t d = (cd.index & 0xFFFF) | (cd.kind << 24);
+      if (cd.kind == kKindInt) {
+        d |= (slot[cd.index] & 0xFF) << 16;
+        if (reach[r]) {
+          if (seen[cd.index]) d |= kStepAccumulate;
+          seen[cd.index] = 1;
+        }
+      }
+      e[1 + j] = d;
+    }
+    int32_t f = 0;
+    if (r == ni - 1) f |= kStepRoot;
+    if (!reach[r]) f |= kStepUnreached;
+    e[3] = f;
+  }
+  if (order.back() != ni - 1) return false;
+  std::memcpy(fwd, enc.data(), enc.size() * sizeof(int32_t));
+
+  // ---- reference backtrack simulation (sankoff.py:212-265) ----
+  // stack of node ids; last_parent[x] / last_slot[x] at x's LAST visit.
+  std::vector<int> last_parent(ni, -1), last_slot(ni, -1);
+  std::vector<char> visited(ni, 0);
+  std::vector<std::pair<int, int>> stk;  // (node, parent*2+slot) ; parent -1 = root entry
+  stk.push_back({n_all - 1, -1});
+  int64_t steps = 0;
+  const int64_t cap = 1LL << 22;
+  bool ok = true;
+  while (!stk.empty()) {
+    if (++steps > cap || (int64_t)stk.size() > 4LL * n_all) { ok = false; break; }
+    auto [node, from] = stk.back();
+    stk.pop_back();
+    if (node < nl) continue;  // leaves and the -1 fill are skipped
+    const int x = node - nl;
+    visited[x] = 1;
+    if (from >= 0) { last_parent[x] = from >> 1; last_slot[x] = from & 1; }
+    const int c0 = ch[2 * node], c1 = ch[2 * node + 1];
+    if (c0 == node || c1 == node) { ok = false; break; }  // self loop: never terminates
+    stk.push_back({c0, 2 * x + 0});
+    stk.push_back({c1, 2 * x + 1});
+  }
+  *bt_ok = ok ? 1 : 0;
+  // process order: BFS over last-parent forest from the root
+  std::vector<std::vector<int>> kidsbt(ni);
+  for (int x = 0; x < ni; ++x)
+    if (ok && visited[x] && last_parent[x] >= 0) kidsbt[last_parent[x]].push_back(x);
+  std::vector<int32_t> benc(2 * ni, 0);
+  int w = 0;
+  if (ok) {
+    std::queue<int> q;
+    q.push(ni - 1);
+    std::vector<char> emitted(ni, 0);
+    while (!q.empty()) {
+      const int x = q.front();
+      q.pop();
+      if (emitted[x]) continue;
+      emitted[x] = 1;
+      int kind, parent = 0;
+      if (x == ni - 1) {
+        kind = kBtRoot;
+      } else {
+        parent = last_parent[x];
+        const int raw = ch[2 * (nl + parent) + last_slot[x]];
+        // the parent's forward used the real row only when raw < parent node
+        kind = (raw < nl + parent) ? kBtReal : kBtSentinel;
+      }
+      benc[2 * w] = (x & 0xFFFF) | (kind << 16) | (last_slot[x] > 0 ? (1 << 20) : 0);
+      benc[2 * w + 1] = parent;
+      ++w;
+      for (int c : kidsbt[x]) q.push(c);
+    }
+    for (int x = 0; x < ni; ++x) {
+      if (!emitted[x]) {
+        benc[2 * w] = (x & 0xFFFF) | (kBtUnreached << 16);
+        benc[2 * w + 1] = 0;
+        ++w;
+      }
+    }
+  }
+  std::memcpy(bt, benc.data(), benc.size() * sizeof(int32_t));
+  return true;
+}
+
+}  // namespace
+
+}  // namespace trex
+
+extern "C" int64_t trex_plan_ints(int B, int n_all) {
+  if (B <= 0 || n_all < 2) return 0;
+  const int ni = n_all - (n_all + 1) / 2;
+  return TREX_PLAN_HEADER_INTS + (int64_t)B * ni * 6;
+}
+
+extern "C" int trex_plan_build(const int32_t* children, int B, int n_all,
+                               int32_t* plan, int32_t* info) {
+  using namespace trex;
+  if (!children || !plan || B <= 0 || n_all < 3 || n_all > 65535)
+    return set_error(TREX_E_ARG, "trex_plan_build: bad arguments (B=%d n_all=%d)", B, n_all);
+  const int nl = (n_all + 1) / 2;
+  const int ni = n_all - nl;
+  std::memset(plan, 0, sizeof(int32_t) * TREX_PLAN_HEADER_INTS);
+  int32_t* fwd = plan + TREX_PLAN_HEADER_INTS;
+  int32_t* bt = fwd + (int64_t)B * ni * 4;
+  int max_slots = 0, all_bt_ok = 1, dag = 0, unr = 0;
+  for (int b = 0; b < B; ++b) {
+    int s = 0, ok = 0, d = 0, u = 0;
+    if (!plan_one_tree(children + (int64_t)b * n_all * 2, n_all, fwd + (int64_t)b * ni * 4,
+                       bt + (int64_t)b * ni * 2, &s, &ok, &d, &u))
+      return set_error(TREX_E_TOPOLOGY, "trex_plan_build: tree %d has an invalid child list", b);
+    max_slots = std::max(max_slots, s);
+    all_bt_ok &= ok;
+    dag += d;
+    unr += u;
+  }
+  plan[0] = kPlanMagic;
+  plan[1] = B;
+  plan[2] = n_all;
+  plan[3] = nl;
+  plan[4] = ni;
+  plan[5] = max_slots;
+  plan[6] = all_bt_ok;
+  if (info) {
+    info[0] = max_slots;
+    info[1] = all_bt_ok;
+    info[2] = dag;
+    info[3] = unr;
+  }
+  return TREX_OK;
+}
