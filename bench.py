@@ -1,0 +1,307 @@
+#!/usr/bin/env python
+"""Benchmark: batched Sankoff forward + gradient on MI355X (BASELINE.json metric).
+
+One step = softmin Sankoff forward (writes the DP table, as trex's run_sankoff
+returns it) + adjoint sweep (d score / d cost) over this rank's shard of the
+C4 workload (BASELINE.json configs[3]: random 32-taxa topologies x 5000 sites
+x 4 states, tau = 0.5), then an RCCL all-reduce of [d_cost, loss] when N > 1.
+Weak scaling: each rank owns --trees-per-gpu trees (default 128, so N = 8 is
+exactly C4's 1024 trees).  Metric: site-node-state updates/s = B*L*n_int*Q per
+step over all ranks.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--trees-per-gpu", type=int, default=128)
+    ap.add_argument("--taxa", type=int, default=32)
+    ap.add_argument("--sites", type=int, default=5000)
+    ap.add_argument("--states", type=int, default=4)
+    ap.add_argument("--tau", type=float, default=0.5)
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly, no hipGraph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 single-tree line")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (written by profiles/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def make_inputs(torch, device, B, n, L, Q, rank):
+    from trex_amd import TreePlan, random_topologies
+
+    ch = random_topologies(B, n, seed=4 + 1000 * rank)
+    plan = TreePlan(ch)
+    g = torch.Generator(device=device)
+    g.manual_seed(5 + 1000 * rank)
+    leaves = torch.randint(0, Q, (B, n, L), generator=g, device=device, dtype=torch.int8)
+    cost = (torch.ones(Q, Q) - torch.eye(Q)).to(device=device, dtype=torch.float32)
+    return ch, plan, leaves, cost
+
+
+class Step:
+    """fwd + adjoint into preallocated buffers (capturable)."""
+
+    def __init__(self, torch, eng, leaves, cost, tau):
+        self.eng, self.leaves, self.cost, self.tau = eng, leaves, cost, tau
+        dev = eng.device
+        self.out_f = {
+            "dp": torch.empty(eng.dp_shape, dtype=torch.float32, device=dev),
+            "tree_score": torch.empty((eng.plan.B,), dtype=torch.float32, device=dev),
+        }
+        self.out_b = {"d_cost": torch.empty((eng.Q, eng.Q), dtype=torch.float32, device=dev)}
+
+    def fwd(self):
+        return self.eng.forward(self.leaves, self.cost, self.tau, dp=True, out=self.out_f)
+
+    def bwd(self):
+        return self.eng.backward(self.leaves, self.cost, self.tau, self.out_f["dp"],
+                                 out=self.out_b)
+
+    def __call__(self):
+        self.fwd()
+        self.bwd()
+
+
+def time_kernels(torch, step, iters=20):
+    """Average device time of the fwd and bwd launches (HIP events on the
+    stream they run on: torch's current stream)."""
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(iters)]
+    for i in range(iters):
+        ev[i][0].record()
+        step.fwd()
+        ev[i][1].record()
+        step.bwd()
+        ev[i][2].record()
+    torch.cuda.synchronize()
+    fwd = np.mean([ev[i][0].elapsed_time(ev[i][1]) for i in range(iters)])
+    bwd = np.mean([ev[i][1].elapsed_time(ev[i][2]) for i in range(iters)])
+    return fwd * 1e-3, bwd * 1e-3
+
+
+def c2_line(torch, device, args, cpu_threads):
+    """C2 (BASELINE.json configs[1]): one balanced 64-taxa tree x 10k sites x
+    4 states, softmin fwd+grad (tau 1.0), leaves simulated along the tree."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cases import simulate_leaves
+
+    from trex_amd import SankoffEngine, TreePlan, children_from_adjacency
+
+    seqs, adj = simulate_leaves(64, 10000, 4, 5, seed=1)
+    ch = children_from_adjacency(adj)
+    eng = SankoffEngine(TreePlan(ch), 10000, 4, device)
+    leaves = torch.from_numpy(np.ascontiguousarray(seqs[None, :64])).to(device)
+    cost = (torch.ones(4, 4) - torch.eye(4)).to(device=device, dtype=torch.float32)
+    step = Step(torch, eng, leaves, cost, 1.0)
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for _ in range(10):
+        g.replay()
+    torch.cuda.synchronize()
+    n = 500
+    t0 = time.perf_counter()
+    for _ in range(n):
+        g.replay()
+    torch.cuda.synchronize()
+    gpu_s = (time.perf_counter() - t0) / n
+    units = 10000 * 63 * 4
+    out = {"workload": "C2: balanced 64-taxa tree x 10000 sites x 4 states, softmin tau=1.0 "
+                       "fwd+grad, hipGraph replay", "ms_per_step": gpu_s * 1e3,
+           "value": units / gpu_s}
+    from oracle.cpu_port import fwd_bwd
+
+    fwd_bwd(ch, seqs[None, :64], cost.cpu().numpy(), 1.0, threads=cpu_threads)
+    reps = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        fwd_bwd(ch, seqs[None, :64], cost.cpu().numpy(), 1.0, threads=cpu_threads)
+        reps.append(time.perf_counter() - t0)
+    cpu_s = float(np.median(reps))
+    out["cpu_port_ms"] = cpu_s * 1e3
+    out["speedup_vs_cpu_port"] = cpu_s / gpu_s
+    return out
+
+
+def cpu_baseline(ch, leaves_np, cost_np, tau, L, n, Q, threads):
+    """OpenMP C restatement (oracle/cpu_port.c) on this host's cores, on a
+    bounded sample of the same workload; plus the trex-structure numpy proxy."""
+    from oracle.cpu_port import fwd_bwd
+
+    nb = len(ch)
+    fwd_bwd(ch[:2], leaves_np[:2], cost_np, tau, threads=threads)  # warm
+    reps = []
+    t_end = time.perf_counter() + 20.0
+    while len(reps) < 5 and (not reps or time.perf_counter() < t_end):
+        t0 = time.perf_counter()
+        fwd_bwd(ch, leaves_np, cost_np, tau, threads=threads)
+        reps.append(time.perf_counter() - t0)
+    sec = float(np.median(reps))
+    units = nb * L * (n - 1) * Q
+    base = {"value": units / sec, "unit": "site-node-state updates/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{nb} trees x {L} sites x {n} taxa x {Q} states softmin fwd+grad "
+                      f"(oracle/cpu_port.c, OpenMP, median of {len(reps)})"}
+    # trex-structure numpy proxy (sankoff.py layout: dp + bt tables, hard fwd)
+    from oracle.sankoff_ref import run_sankoff_ref
+    from trex_amd.topology import adjacency_from_children
+
+    adj = adjacency_from_children(ch[:1])[0]
+    seqs = leaves_np[0].astype(np.float32)
+    t0 = time.perf_counter()
+    run_sankoff_ref(adj, cost_np, seqs, 2 * n - 1, Q, n)
+    px = time.perf_counter() - t0
+    base["trex_numpy_proxy"] = {"value": L * (n - 1) * Q / px, "unit": "site-node-state updates/s",
+                                "cores": 1, "sample": f"1 tree x {L} sites hard forward only "
+                                "(oracle/sankoff_ref.run_sankoff_ref, dp+bt tables as trex)"}
+    return base
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from trex_amd import SankoffEngine
+
+    B, n, L, Q, tau = args.trees_per_gpu, args.taxa, args.sites, args.states, args.tau
+    ch, plan, leaves, cost = make_inputs(torch, device, B, n, L, Q, rank)
+    eng = SankoffEngine(plan, L, Q, device)
+    step = Step(torch, eng, leaves, cost, tau)
+    red = torch.zeros(Q * Q + 1, dtype=torch.float32, device=device)
+
+    use_graph = not args.no_graph
+    graph = None
+    step()
+    torch.cuda.synchronize()
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+
+    def run_once():
+        if graph is not None:
+            graph.replay()
+        else:
+            step()
+        if world > 1:
+            red[:Q * Q].copy_(step.out_b["d_cost"].view(-1))
+            red[Q * Q:].copy_(step.out_f["tree_score"].sum().view(1))
+            dist.all_reduce(red)
+
+    for _ in range(args.warmup):
+        run_once()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_once()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    n_int = n - 1
+    units_per_rank = B * L * n_int * Q
+    value = units_per_rank * world * args.steps / el
+
+    # per-kernel device time (HIP events) -> roofline of the dominant kernel
+    fwd_s, bwd_s = time_kernels(torch, step)
+    nl = n
+    fwd_bytes = B * L * (nl + 4 * Q * n_int)  # int8 leaves in, fp32 DP table out
+    bwd_bytes = B * L * (nl + 4 * Q * n_int)  # leaves + DP table back in
+    kern = {"sankoff_fwd": (fwd_s, fwd_bytes), "sankoff_bwd": (bwd_s, bwd_bytes)}
+    dom = max(kern, key=lambda k: kern[k][0])
+    achieved = kern[dom][1] / kern[dom][0] / 1e9
+    traffic = None
+    try:
+        with open(args.traffic) as f:
+            tj = json.load(f)
+        if tj.get("workload_key") == f"{B}x{n}x{L}x{Q}":
+            traffic = tj.get(dom)
+    except (OSError, ValueError):
+        pass
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "per_kernel_us": {k: round(v[0] * 1e6, 2) for k, v in kern.items()},
+                "algorithmic_bytes": {k: v[1] for k, v in kern.items()}}
+
+    result = {
+        "metric": "site-node-state updates/sec (Sankoff fwd+grad)",
+        "value": value,
+        "unit": "site-node-state updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (random coalescent topologies, iid uniform leaf states, C = 1 - I)",
+        "config": {"workload": f"C4 shard per GPU: {B} random {n}-taxa topologies x {L} sites x "
+                               f"{Q} states, softmin tau={tau} fwd (DP table written) + grad; "
+                               f"global batch {B * world} trees"
+                               + ("; RCCL all-reduce of [dC, loss] per step" if world > 1 else ""),
+                   "trees_per_gpu": B, "taxa": n, "sites": L, "states": Q, "tau": tau,
+                   "hipgraph": use_graph, "parallelism": f"tree-batch x{world}"},
+        "roofline": roofline,
+    }
+    if rank == 0 and world == 1:
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(ch, leaves.cpu().numpy(), cost.cpu().numpy(),
+                                                  tau, L, n, Q, threads)
+        if not args.no_c2:
+            result["c2"] = c2_line(torch, device, args, threads)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -200,7 +200,15 @@ def test_softmin_fwd_grad_vs_fp64(device, tau, L, n):
     dc, mg, anc = eng.backward(lv, c, tau, f.dp, marginals=True, anc_states=True)
     np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL,
                                atol=SOFT_RTOL * np.abs(ref["d_cost"]).max())
-    np.testing.assert_allclose(mg.cpu().numpy(), ref["marginals"], atol=2e-5)
+    # per-site marginals are softmax weights of D/tau: fp32 D carries
+    # ~ulp(|D|) error, amplified by 1/tau -> tolerance ~ 8 eps |D|max / tau
+    mtol = max(2e-5, 8 * 1.2e-7 * np.abs(ref["dp"]).max() / tau)
+    np.testing.assert_allclose(mg.cpu().numpy(), ref["marginals"], atol=mtol)
+    # soft ancestral states = argmax marginals wherever the top two differ
+    m = ref["marginals"]
+    top2 = np.sort(m, axis=2)[:, :, -2:, :]
+    clear = (top2[:, :, 1] - top2[:, :, 0]) > 4 * mtol
+    np.testing.assert_array_equal(anc.cpu().numpy()[clear], m.argmax(axis=2)[clear])
 
 
 def test_softmin_missing_leaves_fp32_offset(device):
