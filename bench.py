@@ -61,7 +61,7 @@ def make_inputs(torch, device, B, n, L, Q, rank):
 
 
 class Step:
-    """fwd + adjoint into preallocated buffers (capturable)."""
+    """fused fwd + adjoint into preallocated buffers (capturable)."""
 
     def __init__(self, torch, eng, leaves, cost, tau):
         self.eng, self.leaves, self.cost, self.tau = eng, leaves, cost, tau
@@ -71,6 +71,10 @@ class Step:
             "tree_score": torch.empty((eng.plan.B,), dtype=torch.float32, device=dev),
         }
         self.out_b = {"d_cost": torch.empty((eng.Q, eng.Q), dtype=torch.float32, device=dev)}
+        self.out_fb = dict(self.out_f, **self.out_b)
+
+    def fused(self):
+        return self.eng.fwd_bwd(self.leaves, self.cost, self.tau, out=self.out_fb)
 
     def fwd(self):
         return self.eng.forward(self.leaves, self.cost, self.tau, dp=True, out=self.out_f)
@@ -80,24 +84,26 @@ class Step:
                                  out=self.out_b)
 
     def __call__(self):
-        self.fwd()
-        self.bwd()
+        self.fused()
 
 
 def time_kernels(torch, step, iters=20):
-    """Average device time of the fwd and bwd launches (HIP events on the
-    stream they run on: torch's current stream)."""
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(iters)]
-    for i in range(iters):
-        ev[i][0].record()
-        step.fwd()
-        ev[i][1].record()
-        step.bwd()
-        ev[i][2].record()
-    torch.cuda.synchronize()
-    fwd = np.mean([ev[i][0].elapsed_time(ev[i][1]) for i in range(iters)])
-    bwd = np.mean([ev[i][1].elapsed_time(ev[i][2]) for i in range(iters)])
-    return fwd * 1e-3, bwd * 1e-3
+    """Average device time per launch of the fused kernel and, for reference,
+    of the separate fwd / adjoint kernels (HIP events on the stream they run
+    on: torch's current stream)."""
+    out = {}
+    for name, fn in (("sankoff_fwd_bwd", step.fused), ("sankoff_fwd", step.fwd),
+                     ("sankoff_bwd", step.bwd)):
+        fn()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(iters)]
+        for e0, e1 in ev:
+            e0.record()
+            fn()
+            e1.record()
+        torch.cuda.synchronize()
+        out[name] = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e-3
+    return out
 
 
 def c2_line(torch, device, args, cpu_threads):
@@ -246,13 +252,18 @@ def main():
     units_per_rank = B * L * n_int * Q
     value = units_per_rank * world * args.steps / el
 
-    # per-kernel device time (HIP events) -> roofline of the dominant kernel
-    fwd_s, bwd_s = time_kernels(torch, step)
+    # per-kernel device time (HIP events) -> roofline of the step's kernel
+    kt = time_kernels(torch, step)
     nl = n
-    fwd_bytes = B * L * (nl + 4 * Q * n_int)  # int8 leaves in, fp32 DP table out
-    bwd_bytes = B * L * (nl + 4 * Q * n_int)  # leaves + DP table back in
-    kern = {"sankoff_fwd": (fwd_s, fwd_bytes), "sankoff_bwd": (bwd_s, bwd_bytes)}
-    dom = max(kern, key=lambda k: kern[k][0])
+    # algorithmic HBM bytes per launch (DESIGN.md "Roofline"):
+    #   fused: int8 leaves in + fp32 DP table out (its re-read is a cache-
+    #          resident recompute choice, not algorithmic traffic)
+    #   fwd:   leaves in + DP table out;  bwd: leaves + DP table in
+    fwd_bytes = B * L * (nl + 4 * Q * n_int)
+    kern = {"sankoff_fwd_bwd": (kt["sankoff_fwd_bwd"], fwd_bytes),
+            "sankoff_fwd": (kt["sankoff_fwd"], fwd_bytes),
+            "sankoff_bwd": (kt["sankoff_bwd"], fwd_bytes)}
+    dom = "sankoff_fwd_bwd"
     achieved = kern[dom][1] / kern[dom][0] / 1e9
     traffic = None
     try:

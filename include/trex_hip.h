@@ -68,8 +68,12 @@ int64_t trex_plan_ints(int B, int n_all);
 int trex_plan_build(const int32_t* children, int B, int n_all, int32_t* plan,
                     int32_t* info);
 
-/* Workspace (device bytes) needed by fwd/bwd for a given shape. */
+/* Workspace (device bytes) needed by fwd/bwd for a given shape.  It holds
+ * per-block partial sums and arrival counters for the in-kernel,
+ * fixed-order (bitwise reproducible) reductions; zero it once with
+ * trex_workspace_init before first use (the kernels leave it zeroed). */
 int64_t trex_workspace_bytes(int B, int L, int n_all, int Q);
+int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Forward DP.  Replaces vectorized_dp/run_dp + the total of run_sankoff
@@ -79,7 +83,7 @@ int64_t trex_workspace_bytes(int B, int L, int n_all, int Q);
  *            sankoff.py:50)
  *   cost     fp32  [Q][Q]            substitution cost C[parent][child]
  *   tau      0 => hard min-plus (trex); >0 => softmin relaxation
- *   dp       fp32  [B][n_int][Q][L]  internal rows, or NULL
+ *   dp       fp32  [B][n_int][Q][L]  internal rows (required)
  *   site_score fp32 [B][L] or NULL;  tree_score fp32 [B] (required)
  * ---------------------------------------------------------------------- */
 int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
@@ -105,6 +109,20 @@ int trex_sankoff_bwd(const int32_t* plan, int n_slots, const int8_t* leaves,
                      unsigned flags, const float* dp, const float* d_tree_score,
                      float* d_cost, float* marginals, int8_t* anc_states,
                      void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Fused forward + adjoint in one launch (the benchmark step): writes dp,
+ * tree_score (and site_score / marginals / anc_states when non-NULL) and
+ * d_cost; each wave's adjoint re-reads the DP rows it has just written.
+ * Same arguments and semantics as trex_sankoff_fwd followed by
+ * trex_sankoff_bwd.
+ * ---------------------------------------------------------------------- */
+int trex_sankoff_fwd_bwd(const int32_t* plan, int n_slots, const int8_t* leaves,
+                         const float* cost, int B, int L, int n_all, int Q, float tau,
+                         unsigned flags, float* dp, float* site_score,
+                         float* tree_score, const float* d_tree_score, float* d_cost,
+                         float* marginals, int8_t* anc_states, void* workspace,
+                         int64_t workspace_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Ancestral reconstruction, bit-exact with the reference's backtrack:

@@ -307,3 +307,55 @@ def test_c4_scale_properties(device):
     np.testing.assert_allclose(ds.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
     d3, _, _ = eng.backward(lv, c, tau, f1.dp, torch.full((B,), 3.0, device=device))
     np.testing.assert_allclose(d3.cpu().numpy(), 3.0 * d1.cpu().numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("tau", [0.0, 0.5, 0.05])
+def test_fused_fwd_bwd_equals_separate_launches(device, tau):
+    """trex_sankoff_fwd_bwd == trex_sankoff_fwd + trex_sankoff_bwd, bit for bit
+    (same per-wave arithmetic, same fixed-order reductions)."""
+    B, n, L, Q = 7, 24, 999, 4
+    ch = random_topologies(B, n, seed=21)
+    leaves = random_leaves(B, n, L, Q, seed=22, missing=0.01)
+    cost = int_cost(Q, seed=23, hi=9 if tau == 0.05 else 4)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    dts = torch.linspace(0.5, 2.0, B, device=device)
+    f, dc, mg, an = eng.fwd_bwd(lv, c, tau, dts, site_score=True, marginals=True,
+                                anc_states=True)
+    f2 = eng.forward(lv, c, tau, site_score=True)
+    dc2, mg2, an2 = eng.backward(lv, c, tau, f2.dp, dts, marginals=True, anc_states=True)
+    assert torch.equal(f.dp, f2.dp)
+    assert torch.equal(f.tree_score, f2.tree_score)
+    assert torch.equal(f.site_score, f2.site_score)
+    assert torch.equal(dc, dc2) and torch.equal(mg, mg2) and torch.equal(an, an2)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, tau, d_tree_score=dts.cpu().numpy())
+    if tau == 0.0:
+        np.testing.assert_array_equal(f.tree_score.cpu().numpy(),
+                                      ref["tree_score"].astype(np.float32))
+        np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=1e-6)
+    else:
+        np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
+
+
+def test_repeated_launches_reset_reduction_counters(device):
+    """The in-kernel reductions leave their arrival counters at zero, so
+    back-to-back launches (and hipGraph replays) keep producing the same sums."""
+    B, n, L, Q = 33, 16, 300, 4
+    ch = random_topologies(B, n, seed=31)
+    leaves = random_leaves(B, n, L, Q, seed=32)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(hamming(Q), device, torch.float32)
+    f0, d0, _, _ = eng.fwd_bwd(lv, c, 0.5)
+    t0, dd0 = f0.tree_score.clone(), d0.clone()
+    g = torch.cuda.CUDAGraph()
+    out = {"dp": f0.dp, "tree_score": f0.tree_score, "d_cost": d0}
+    with torch.cuda.graph(g):
+        eng.fwd_bwd(lv, c, 0.5, out=out)
+    for _ in range(5):
+        out["tree_score"].zero_()
+        out["d_cost"].zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out["tree_score"], t0) and torch.equal(out["d_cost"], dd0)

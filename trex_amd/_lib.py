@@ -39,6 +39,9 @@ SIGNATURES = {
                                 _p, _p, _p, _p, _c_i64, _p]),
     "trex_sankoff_bwd": (_c_i, [_p, _c_i, _p, _p, _c_i, _c_i, _c_i, _c_i, _c_f, _c_u,
                                 _p, _p, _p, _p, _p, _p, _c_i64, _p]),
+    "trex_workspace_init": (_c_i, [_p, _c_i64, _p]),
+    "trex_sankoff_fwd_bwd": (_c_i, [_p, _c_i, _p, _p, _c_i, _c_i, _c_i, _c_i, _c_f, _c_u,
+                                    _p, _p, _p, _p, _p, _p, _p, _p, _c_i64, _p]),
     "trex_sankoff_backtrack": (_c_i, [_p, _c_i, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
     "trex_dp_to_trex_layout": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
 }

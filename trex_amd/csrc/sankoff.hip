@@ -27,7 +27,7 @@ thread_local char g_err[512] = "no error";
 
 constexpr float kSentinel = 1e5f;  // sankoff.py:152
 constexpr int kWave = 64;
-constexpr int kKindSent = 0, kKindLeaf = 1, kKindInt = 2;
+constexpr int kKindLeaf = 1, kKindInt = 2;  // 0 = 1e5 sentinel row
 
 // --------------------------------------------------------------------------
 // per-lane vector helpers (SPT consecutive sites per lane)
@@ -85,6 +85,23 @@ __device__ __forceinline__ void st_codes(int8_t* __restrict__ p, const int (&c)[
   }
 }
 
+// Read-only, wave-uniform data (topology program, cost matrix) goes through
+// the constant address space so hipcc emits scalar loads (s_load): vector
+// loads would be ordered behind the wave's in-flight DP-table stores in vmcnt.
+template <class T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <class T>
+__device__ __forceinline__ cptr<T> as_const(const T* p) {
+  return (cptr<T>)(p);
+}
+
+struct I4 {
+  int x, y, z, w;
+};
+__device__ __forceinline__ I4 load_step(cptr<int> prog, int k) {
+  return I4{prog[4 * k], prog[4 * k + 1], prog[4 * k + 2], prog[4 * k + 3]};
+}
+
 __device__ __forceinline__ float uniform(float x) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
@@ -93,38 +110,53 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 __device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
 
 // --------------------------------------------------------------------------
-// cost matrix in SGPRs; K[i][j] = exp(-(C[i][j]-cmin)/tau) for the softmin
+// cost matrix in SGPRs.  MODE: kHard (min-plus), kSoftK (factored softmin,
+// K[i][j] = exp(-(C[i][j]-cmin)/tau) in SGPRs), kSoftDirect (per-row
+// stabilised softmin, used when range(C)/tau > 40 would underflow K).
 // --------------------------------------------------------------------------
+constexpr int kHard = 0, kSoftK = 1, kSoftDirect = 2;
+
 template <int Q>
 struct Coef {
   float c[Q][Q];
   float k[Q][Q];
   float cmin;
-  bool ktrick;  // all K >= exp(-40): the factored softmin is exact to fp32
 };
 
-template <int Q, bool SOFT>
-__device__ __forceinline__ void load_coef(const float* __restrict__ cost, float a, Coef<Q>& cf) {
-  float cmin = INFINITY, cmax = -INFINITY;
+// range(C)/tau <= 40: the factored form keeps every K >= e^-40
+__device__ __forceinline__ bool use_ktrick(float cmin, float cmax, float a) {
+  return (cmax - cmin) * a <= 57.70780f;  // log2(e^40)
+}
+
+template <int Q>
+__device__ __forceinline__ void cost_range(const float* __restrict__ cost_, float& cmin,
+                                           float& cmax) {
+  const cptr<float> cost = as_const(cost_);
+  cmin = INFINITY;
+  cmax = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < Q * Q; ++q) {
+    const float v = cost[q];
+    cmin = fminf(cmin, v);
+    cmax = fmaxf(cmax, v);
+  }
+  cmin = uniform(cmin);
+  cmax = uniform(cmax);
+}
+
+template <int Q, int MODE>
+__device__ __forceinline__ void load_coef(const float* __restrict__ cost_, float a, Coef<Q>& cf) {
+  float cmax;
+  cost_range<Q>(cost_, cf.cmin, cmax);
+  const cptr<float> cost = as_const(cost_);
 #pragma unroll
   for (int i = 0; i < Q; ++i)
 #pragma unroll
     for (int j = 0; j < Q; ++j) {
-      const float v = uniform(cost[i * Q + j]);
+      const float v = cost[i * Q + j];
       cf.c[i][j] = v;
-      cmin = fminf(cmin, v);
-      cmax = fmaxf(cmax, v);
+      if constexpr (MODE == kSoftK) cf.k[i][j] = uniform(fast_exp2((cf.cmin - v) * a));
     }
-  cf.cmin = uniform(cmin);
-  cf.ktrick = false;
-  if constexpr (SOFT) {
-    // log2(e^40) = 57.7: range/tau <= 40
-    cf.ktrick = (cmax - cmin) * a <= 57.70780f;
-#pragma unroll
-    for (int i = 0; i < Q; ++i)
-#pragma unroll
-      for (int j = 0; j < Q; ++j) cf.k[i][j] = uniform(fast_exp2((cf.cmin - cf.c[i][j]) * a));
-  }
 }
 
 // --------------------------------------------------------------------------
@@ -148,25 +180,114 @@ __device__ __forceinline__ void fill_sentinel(float (&d)[Q][SPT]) {
     for (int s = 0; s < SPT; ++s) d[j][s] = kSentinel;
 }
 
+// LDS slot stack: [slot][lane][Q][SPT] -- each lane's vector is contiguous,
+// so a slot access is Q*SPT/4 ds_read_b128 / ds_write_b128.
+template <int N>
+__device__ __forceinline__ void lds_vec_get(const float* p, float (&o)[N]) {
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int t = 0; t < N / 4; ++t) {
+      const float4 v = reinterpret_cast<const float4*>(p)[t];
+      o[4 * t] = v.x; o[4 * t + 1] = v.y; o[4 * t + 2] = v.z; o[4 * t + 3] = v.w;
+    }
+  } else if constexpr (N % 2 == 0) {
+#pragma unroll
+    for (int t = 0; t < N / 2; ++t) {
+      const float2 v = reinterpret_cast<const float2*>(p)[t];
+      o[2 * t] = v.x; o[2 * t + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < N; ++t) o[t] = p[t];
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void lds_vec_put(float* p, const float (&o)[N]) {
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int t = 0; t < N / 4; ++t)
+      reinterpret_cast<float4*>(p)[t] = make_float4(o[4 * t], o[4 * t + 1], o[4 * t + 2], o[4 * t + 3]);
+  } else if constexpr (N % 2 == 0) {
+#pragma unroll
+    for (int t = 0; t < N / 2; ++t) reinterpret_cast<float2*>(p)[t] = make_float2(o[2 * t], o[2 * t + 1]);
+  } else {
+#pragma unroll
+    for (int t = 0; t < N; ++t) p[t] = o[t];
+  }
+}
+
 template <int Q, int SPT>
 __device__ __forceinline__ void lds_get(const float* lds, int slot, int lane, float (&d)[Q][SPT]) {
+  float buf[Q * SPT];
+  lds_vec_get<Q * SPT>(lds + (slot * kWave + lane) * (Q * SPT), buf);
 #pragma unroll
-  for (int j = 0; j < Q; ++j) ld<SPT>(lds + ((slot * Q + j) * kWave + lane) * SPT, d[j]);
+  for (int j = 0; j < Q; ++j)
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) d[j][s] = buf[j * SPT + s];
 }
 
 template <int Q, int SPT>
 __device__ __forceinline__ void lds_put(float* lds, int slot, int lane, const float (&d)[Q][SPT]) {
+  float buf[Q * SPT];
 #pragma unroll
-  for (int j = 0; j < Q; ++j) st<SPT>(lds + ((slot * Q + j) * kWave + lane) * SPT, d[j]);
+  for (int j = 0; j < Q; ++j)
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) buf[j * SPT + s] = d[j][s];
+  lds_vec_put<Q * SPT>(lds + (slot * kWave + lane) * (Q * SPT), buf);
+}
+
+// C[i][code] from SGPR operands (code in [0, Q)); bit-tree select on SSA values
+template <int Q>
+__device__ __forceinline__ float pick(const float (&row)[Q], int code) {
+  float r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = row[j < Q ? j : 0];
+  const bool b0 = (code & 1) != 0;
+  const float lo = b0 ? r[1] : r[0];
+  if constexpr (Q == 2) return lo;
+  if constexpr (Q == 3) return (code & 2) ? r[2] : lo;
+  const float hi = b0 ? r[3] : r[2];
+  return (code & 2) ? hi : lo;
+}
+
+// ---- buffer (SRD) access: 32-bit lane offset in voffset, row offset in
+// soffset, no 64-bit VALU address arithmetic per access ----
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+template <int SPT>
+__device__ __forceinline__ void bst(rsrc_t r, int voff, int soff, const float (&o)[SPT]) {
+  if constexpr (SPT == 2) {
+    u32x2 w = {__float_as_uint(o[0]), __float_as_uint(o[1])};
+    __builtin_amdgcn_raw_buffer_store_b64(w, r, voff, soff, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o[0]), r, voff, soff, 0);
+  }
+}
+
+template <int SPT>
+__device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT]) {
+  if constexpr (SPT == 2) {
+    const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    o[0] = __uint_as_float(w.x);
+    o[1] = __uint_as_float(w.y);
+  } else {
+    o[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  }
 }
 
 // --------------------------------------------------------------------------
 // message M_c[i] = min_j / smin_j (C[i][j] + D_c[j])      (sankoff.py:67-68)
 // --------------------------------------------------------------------------
-template <int Q, int SPT, bool SOFT>
+template <int Q, int SPT, int MODE>
 __device__ __forceinline__ void message(const Coef<Q>& cf, float a, float bcoef,
                                         const float (&d)[Q][SPT], float (&m)[Q][SPT]) {
-  if constexpr (!SOFT) {
+  if constexpr (MODE == kHard) {
 #pragma unroll
     for (int i = 0; i < Q; ++i)
 #pragma unroll
@@ -176,43 +297,41 @@ __device__ __forceinline__ void message(const Coef<Q>& cf, float a, float bcoef,
         for (int j = 1; j < Q; ++j) v = fminf(v, cf.c[i][j] + d[j][s]);
         m[i][s] = v;
       }
+  } else if constexpr (MODE == kSoftK) {
+#pragma unroll
+    for (int s = 0; s < SPT; ++s) {
+      float md = d[0][s];
+#pragma unroll
+      for (int j = 1; j < Q; ++j) md = fminf(md, d[j][s]);
+      float u[Q];
+#pragma unroll
+      for (int j = 0; j < Q; ++j) u[j] = fast_exp2((md - d[j][s]) * a);
+      const float base = md + cf.cmin;
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        float acc = cf.k[i][0] * u[0];
+#pragma unroll
+        for (int j = 1; j < Q; ++j) acc = fmaf(cf.k[i][j], u[j], acc);
+        m[i][s] = fmaf(-bcoef, fast_log2(acc), base);
+      }
+    }
   } else {
-    if (cf.ktrick) {
+#pragma unroll
+    for (int i = 0; i < Q; ++i)
 #pragma unroll
       for (int s = 0; s < SPT; ++s) {
-        float md = d[0][s];
+        float x[Q];
+        float mn = INFINITY;
 #pragma unroll
-        for (int j = 1; j < Q; ++j) md = fminf(md, d[j][s]);
-        float u[Q];
-#pragma unroll
-        for (int j = 0; j < Q; ++j) u[j] = fast_exp2((md - d[j][s]) * a);
-        const float base = md + cf.cmin;
-#pragma unroll
-        for (int i = 0; i < Q; ++i) {
-          float acc = cf.k[i][0] * u[0];
-#pragma unroll
-          for (int j = 1; j < Q; ++j) acc = fmaf(cf.k[i][j], u[j], acc);
-          m[i][s] = base - bcoef * fast_log2(acc);
+        for (int j = 0; j < Q; ++j) {
+          x[j] = cf.c[i][j] + d[j][s];
+          mn = fminf(mn, x[j]);
         }
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < Q; ++j) acc += fast_exp2((mn - x[j]) * a);
+        m[i][s] = fmaf(-bcoef, fast_log2(acc), mn);
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < Q; ++i)
-#pragma unroll
-        for (int s = 0; s < SPT; ++s) {
-          float x[Q];
-          float mn = INFINITY;
-#pragma unroll
-          for (int j = 0; j < Q; ++j) {
-            x[j] = cf.c[i][j] + d[j][s];
-            mn = fminf(mn, x[j]);
-          }
-          float acc = 0.0f;
-#pragma unroll
-          for (int j = 0; j < Q; ++j) acc += fast_exp2((mn - x[j]) * a);
-          m[i][s] = mn - bcoef * fast_log2(acc);
-        }
-    }
   }
 }
 
@@ -222,16 +341,16 @@ __device__ __forceinline__ void message(const Coef<Q>& cf, float a, float bcoef,
 // In the factored softmin acc holds sum r_i u_j; the K[i][j] factor is
 // applied once in the final reduction.
 // --------------------------------------------------------------------------
-template <int Q, int SPT, bool SOFT, bool WANT_GC>
+template <int Q, int SPT, int MODE>
 __device__ __forceinline__ void message_adjoint(const Coef<Q>& cf, float a,
                                                 const float (&d)[Q][SPT],
                                                 const float (&g)[Q][SPT],
                                                 float (&acc)[Q][Q], float (&gc)[Q][SPT]) {
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
+    if constexpr (MODE == kHard) {
 #pragma unroll
-    for (int j = 0; j < Q; ++j) gc[j][s] = 0.0f;
-    if constexpr (!SOFT) {
+      for (int j = 0; j < Q; ++j) gc[j][s] = 0.0f;
 #pragma unroll
       for (int i = 0; i < Q; ++i) {
         float x[Q];
@@ -250,62 +369,60 @@ __device__ __forceinline__ void message_adjoint(const Coef<Q>& cf, float a,
         for (int j = 0; j < Q; ++j) {
           const float w = (x[j] == mn) ? r : 0.0f;
           acc[i][j] += w;
-          if constexpr (WANT_GC) gc[j][s] += w;
+          gc[j][s] += w;
         }
       }
+    } else if constexpr (MODE == kSoftK) {
+      float md = d[0][s];
+#pragma unroll
+      for (int j = 1; j < Q; ++j) md = fminf(md, d[j][s]);
+      float u[Q];
+#pragma unroll
+      for (int j = 0; j < Q; ++j) u[j] = fast_exp2((md - d[j][s]) * a);
+      float r[Q];
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        float sm = cf.k[i][0] * u[0];
+#pragma unroll
+        for (int j = 1; j < Q; ++j) sm = fmaf(cf.k[i][j], u[j], sm);
+        r[i] = g[i][s] * __builtin_amdgcn_rcpf(sm);
+      }
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int j = 0; j < Q; ++j) acc[i][j] = fmaf(r[i], u[j], acc[i][j]);
+#pragma unroll
+      for (int j = 0; j < Q; ++j) {
+        float t = r[0] * cf.k[0][j];
+#pragma unroll
+        for (int i = 1; i < Q; ++i) t = fmaf(r[i], cf.k[i][j], t);
+        gc[j][s] = u[j] * t;
+      }
     } else {
-      if (cf.ktrick) {
-        float md = d[0][s];
 #pragma unroll
-        for (int j = 1; j < Q; ++j) md = fminf(md, d[j][s]);
-        float u[Q];
+      for (int j = 0; j < Q; ++j) gc[j][s] = 0.0f;
 #pragma unroll
-        for (int j = 0; j < Q; ++j) u[j] = fast_exp2((md - d[j][s]) * a);
-        float r[Q];
+      for (int i = 0; i < Q; ++i) {
+        float x[Q];
+        float mn = INFINITY;
 #pragma unroll
-        for (int i = 0; i < Q; ++i) {
-          float sm = cf.k[i][0] * u[0];
-#pragma unroll
-          for (int j = 1; j < Q; ++j) sm = fmaf(cf.k[i][j], u[j], sm);
-          r[i] = g[i][s] * __builtin_amdgcn_rcpf(sm);
+        for (int j = 0; j < Q; ++j) {
+          x[j] = cf.c[i][j] + d[j][s];
+          mn = fminf(mn, x[j]);
         }
+        float e[Q];
+        float sm = 0.0f;
 #pragma unroll
-        for (int i = 0; i < Q; ++i)
-#pragma unroll
-          for (int j = 0; j < Q; ++j) acc[i][j] = fmaf(r[i], u[j], acc[i][j]);
-        if constexpr (WANT_GC) {
-#pragma unroll
-          for (int j = 0; j < Q; ++j) {
-            float t = r[0] * cf.k[0][j];
-#pragma unroll
-            for (int i = 1; i < Q; ++i) t = fmaf(r[i], cf.k[i][j], t);
-            gc[j][s] = u[j] * t;
-          }
+        for (int j = 0; j < Q; ++j) {
+          e[j] = fast_exp2((mn - x[j]) * a);
+          sm += e[j];
         }
-      } else {
+        const float r = g[i][s] * __builtin_amdgcn_rcpf(sm);
 #pragma unroll
-        for (int i = 0; i < Q; ++i) {
-          float x[Q];
-          float mn = INFINITY;
-#pragma unroll
-          for (int j = 0; j < Q; ++j) {
-            x[j] = cf.c[i][j] + d[j][s];
-            mn = fminf(mn, x[j]);
-          }
-          float e[Q];
-          float sm = 0.0f;
-#pragma unroll
-          for (int j = 0; j < Q; ++j) {
-            e[j] = fast_exp2((mn - x[j]) * a);
-            sm += e[j];
-          }
-          const float r = g[i][s] * __builtin_amdgcn_rcpf(sm);
-#pragma unroll
-          for (int j = 0; j < Q; ++j) {
-            const float w = r * e[j];
-            acc[i][j] += w;
-            if constexpr (WANT_GC) gc[j][s] += w;
-          }
+        for (int j = 0; j < Q; ++j) {
+          const float w = r * e[j];
+          acc[i][j] += w;
+          gc[j][s] += w;
         }
       }
     }
@@ -340,7 +457,7 @@ __device__ __forceinline__ void root_score(const float (&d)[Q][SPT], float a, fl
       const float r = __builtin_amdgcn_rcpf(sm);
 #pragma unroll
       for (int i = 0; i < Q; ++i) w[i][s] *= r;
-      score[s] = mn - bcoef * fast_log2(sm);
+      score[s] = fmaf(-bcoef, fast_log2(sm), mn);
     }
   }
 }
@@ -352,178 +469,423 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // --------------------------------------------------------------------------
-// forward kernel
+// Unified Sankoff kernel: PHASE 1 = forward, 2 = adjoint, 3 = both (fused).
+//
+// One wave per workgroup = 64*SPT consecutive sites of one tree.  LDS holds
+//   [slots][Q][64][SPT] f32  live D vectors (forward) / cotangents (adjoint)
+//   [nl][64][SPT]       i8   the tile's leaf states (prologue prefetch)
+// Leaf messages take the exact closed form C[i][code] whenever the 1e5
+// sentinel dominates (hard: range(C) < 1e5; soft: exp(-(1e5-range)/tau) <
+// 2^-64), i.e. no transcendental for half of all children.
 // --------------------------------------------------------------------------
-template <int Q, int SPT, bool SOFT>
-__global__ __launch_bounds__(kWave) void sankoff_fwd_kernel(
-    const int4* __restrict__ steps, const int8_t* __restrict__ leaves,
-    const float* __restrict__ cost, int n_int, int nl, int L, int tiles, float a, float bcoef,
-    int hard_root, float* __restrict__ dp, float* __restrict__ site_score,
-    double* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tree = blockIdx.x / tiles;
-  const int tile = blockIdx.x - tree * tiles;
-  const int lane = threadIdx.x;
-  const int site = (tile * kWave + lane) * SPT;
-  const bool active = site < L;
-  const int sc = active ? site : 0;
+struct KArgs {
+  const int4* steps;
+  const int8_t* leaves;
+  const float* cost;
+  int n_int, nl, L, tiles, B, n_slots;
+  float a, bcoef;
+  int hard_root;
+  float* dp;            // [B][n_int][Q][L] (fwd writes / adjoint reads)
+  float* site_score;    // [B][L] or null
+  float* tree_score;    // [B]
+  const float* dts;     // [B] or null
+  float* marg;          // [B][n_int][Q][L] or null
+  int8_t* anc;          // [B][n_int][L] or null
+  float* d_cost;        // [Q][Q]
+  double* part_tree;    // [B*tiles]
+  double* part_dc;      // [Q*Q][B*tiles]
+  double* tree_dc;      // [Q*Q][B]
+  int* counters;        // [B+1], zero at rest (self-resetting)
+};
 
-  Coef<Q> cf;
-  load_coef<Q, SOFT>(cost, a, cf);
-
-  const int4* prog = steps + (size_t)tree * n_int;
-  const int8_t* lv = leaves + (size_t)tree * nl * L + sc;
-  const size_t rowstride = (size_t)Q * L;
-  float* dpt = dp ? dp + (size_t)tree * n_int * rowstride + sc : nullptr;
-
-  float dv[Q][SPT];
-  for (int k = 0; k < n_int; ++k) {
-    const int4 stp = prog[k];
-    float d[Q][SPT], m[Q][SPT];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int desc = c == 0 ? stp.y : stp.z;
-      const int kind = (desc >> 24) & 3;
-      if (kind == kKindLeaf) {
-        leaf_rows<Q, SPT>(lv + (size_t)(desc & 0xFFFF) * L, d);
-      } else if (kind == kKindInt) {
-        lds_get<Q, SPT>(lds, (desc >> 16) & 0xFF, lane, d);
-      } else {
-        fill_sentinel<Q, SPT>(d);
-      }
-      message<Q, SPT, SOFT>(cf, a, bcoef, d, m);
-#pragma unroll
-      for (int i = 0; i < Q; ++i)
-#pragma unroll
-        for (int s = 0; s < SPT; ++s) dv[i][s] = (c == 0) ? m[i][s] : dv[i][s] + m[i][s];
-    }
-    const int row = stp.x & 0xFFFF;
-    const int oslot = (stp.x >> 16) & 0xFF;
-    if (dpt && active) {
-#pragma unroll
-      for (int i = 0; i < Q; ++i) st<SPT>(dpt + (size_t)row * rowstride + (size_t)i * L, dv[i]);
-    }
-    if (oslot != 0xFF) lds_put<Q, SPT>(lds, oslot, lane, dv);
-  }
-  // the root is the last step (plan.cpp)
-  float score[SPT], w[Q][SPT];
-  root_score<Q, SPT, SOFT>(dv, a, bcoef, hard_root != 0, score, w);
-  double tot = 0.0;
-  if (active) {
-#pragma unroll
-    for (int s = 0; s < SPT; ++s) tot += (double)score[s];
-    if (site_score) st<SPT>(site_score + (size_t)tree * L + site, score);
-  }
-  tot = wave_sum(tot);
-  if (lane == 0) part[blockIdx.x] = tot;
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// --------------------------------------------------------------------------
-// adjoint (reverse) kernel
-// --------------------------------------------------------------------------
-template <int Q, int SPT, bool SOFT>
-__global__ __launch_bounds__(kWave) void sankoff_bwd_kernel(
-    const int4* __restrict__ steps, const int8_t* __restrict__ leaves,
-    const float* __restrict__ cost, int n_int, int nl, int L, int tiles, float a, float bcoef,
-    int hard_root, const float* __restrict__ dp, const float* __restrict__ dts,
-    float* __restrict__ marg, int8_t* __restrict__ anc, double* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tree = blockIdx.x / tiles;
-  const int tile = blockIdx.x - tree * tiles;
+// sum of n values (lane-strided, fixed order) -> every lane
+__device__ __forceinline__ double wave_sum_strided(const double* p, int n, int lane) {
+  double v = 0.0;
+  for (int t = lane; t < n; t += kWave) v += load_sc1(p + t);
+  return wave_sum(v);
+}
+
+// LDS map (floats): [0, 64) leaf tables: T[code][i] (message; code Q =
+// missing leaf) at 0, IK[code][i] = 1/K[i][code] (factored-form leaf adjoint
+// weight) at 32; then slots [n_slots + 2][64][Q*SPT] (n_slots = root cotangent,
+// n_slots + 1 = all-1e5 sentinel row), then the leaf tile [nl][64][SPT] i8.
+constexpr int kTabFloats = 64;
+
+template <int Q, int SPT, int MODE, int PHASE, bool LFAST>
+__device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
+  constexpr bool SOFT = MODE != kHard;
+  constexpr bool FWD = (PHASE & 1) != 0;
+  constexpr bool BWD = (PHASE & 2) != 0;
+  const int tree = blockIdx.x / A.tiles;
+  const int tile = blockIdx.x - tree * A.tiles;
   const int lane = threadIdx.x;
   const int site = (tile * kWave + lane) * SPT;
-  const bool active = site < L;
+  const bool active = site < A.L;
   const int sc = active ? site : 0;
+  const int L = A.L;
+  const float a = A.a, bcoef = A.bcoef;
 
   Coef<Q> cf;
-  load_coef<Q, SOFT>(cost, a, cf);
-  const float dscale = dts ? uniform(dts[tree]) : 1.0f;
+  load_coef<Q, MODE>(A.cost, a, cf);
 
-  const int4* prog = steps + (size_t)tree * n_int;
-  const int8_t* lv = leaves + (size_t)tree * nl * L + sc;
-  const size_t rowstride = (size_t)Q * L;
-  const float* dpt = dp + (size_t)tree * n_int * rowstride + sc;
-  float* mt = marg ? marg + (size_t)tree * n_int * rowstride + sc : nullptr;
-  int8_t* at = anc ? anc + (size_t)tree * n_int * L + sc : nullptr;
+  float* tab = lds;
+  float* slots = lds + kTabFloats;
+  const int kRootSlot = A.n_slots, kSentSlot = A.n_slots + 1;
+  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 2) * Q * kWave * SPT);
 
-  float acc[Q][Q];
+  // ---- prologue ----
+  {
+    // leaf message table: T[s][i] = C[i][s]; T[Q][i] = message of an all-1e5 row
+    if (lane < Q) {
+      float d1[Q][1], m1[Q][1];
 #pragma unroll
-  for (int i = 0; i < Q; ++i)
-#pragma unroll
-    for (int j = 0; j < Q; ++j) acc[i][j] = 0.0f;
-
-  for (int k = n_int - 1; k >= 0; --k) {
-    const int4 stp = prog[k];
-    if (stp.w & kStepUnreached) continue;
-    const int row = stp.x & 0xFFFF;
-    float g[Q][SPT];
-    if (stp.w & kStepRoot) {
-      float d[Q][SPT], score[SPT];
-#pragma unroll
-      for (int i = 0; i < Q; ++i) ld<SPT>(dpt + (size_t)row * rowstride + (size_t)i * L, d[i]);
-      root_score<Q, SPT, SOFT>(d, a, bcoef, hard_root != 0, score, g);
-      const float f = active ? dscale : 0.0f;
+      for (int j = 0; j < Q; ++j) d1[j][0] = kSentinel;
+      message<Q, 1, MODE>(cf, a, bcoef, d1, m1);
 #pragma unroll
       for (int i = 0; i < Q; ++i)
+        if (i == lane) tab[Q * Q + i] = m1[i][0];
 #pragma unroll
-        for (int s = 0; s < SPT; ++s) g[i][s] *= f;
-    } else {
-      lds_get<Q, SPT>(lds, (stp.x >> 16) & 0xFF, lane, g);
-    }
-    if (mt && active) {
-#pragma unroll
-      for (int i = 0; i < Q; ++i) st<SPT>(mt + (size_t)row * rowstride + (size_t)i * L, g[i]);
-    }
-    if (at && active) {
-      int best[SPT];
-#pragma unroll
-      for (int s = 0; s < SPT; ++s) {
-        float bv = g[0][s];
-        int bi = 0;
-#pragma unroll
-        for (int i = 1; i < Q; ++i)
-          if (g[i][s] > bv) { bv = g[i][s]; bi = i; }
-        best[s] = bi;
+      for (int st_ = 0; st_ < Q; ++st_) {
+        const float cv = as_const(A.cost)[lane * Q + st_];
+        tab[st_ * Q + lane] = cv;
+        if constexpr (MODE == kSoftK) tab[32 + st_ * Q + lane] = fast_exp2((cv - cf.cmin) * a);
       }
-      st_codes<SPT>(at + (size_t)row * L, best);
     }
+    float sent[Q][SPT];
+    fill_sentinel<Q, SPT>(sent);
+    lds_put<Q, SPT>(slots, kSentSlot, lane, sent);
+    // leaf tile: codes normalised to [0, Q] (Q = trex's dropped scatter)
+    const int8_t* lv = A.leaves + (size_t)tree * A.nl * L + sc;
+    constexpr int kBatch = 16;
+    for (int c0 = 0; c0 < A.nl; c0 += kBatch) {
+      int code[kBatch][SPT];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int desc = c == 0 ? stp.y : stp.z;
-      const int kind = (desc >> 24) & 3;
-      float d[Q][SPT], gc[Q][SPT];
-      if (kind == kKindLeaf) {
-        leaf_rows<Q, SPT>(lv + (size_t)(desc & 0xFFFF) * L, d);
-        message_adjoint<Q, SPT, SOFT, false>(cf, a, d, g, acc, gc);
-      } else if (kind == kKindInt) {
-        const int crow = desc & 0xFFFF;
+      for (int u = 0; u < kBatch; ++u)
+        if (c0 + u < A.nl) ld_codes<SPT>(lv + (size_t)(c0 + u) * L, code[u]);
 #pragma unroll
-        for (int j = 0; j < Q; ++j) ld<SPT>(dpt + (size_t)crow * rowstride + (size_t)j * L, d[j]);
-        message_adjoint<Q, SPT, SOFT, true>(cf, a, d, g, acc, gc);
-        const int cslot = (desc >> 16) & 0xFF;
-        if (desc & kStepAccumulate) {
-          float old[Q][SPT];
-          lds_get<Q, SPT>(lds, cslot, lane, old);
+      for (int u = 0; u < kBatch; ++u) {
+        if (c0 + u < A.nl) {
 #pragma unroll
-          for (int j = 0; j < Q; ++j)
-#pragma unroll
-            for (int s = 0; s < SPT; ++s) gc[j][s] += old[j][s];
+          for (int s = 0; s < SPT; ++s) code[u][s] = ((unsigned)code[u][s] < (unsigned)Q) ? code[u][s] : Q;
+          st_codes<SPT>(lleaf + ((c0 + u) * kWave + lane) * SPT, code[u]);
         }
-        lds_put<Q, SPT>(lds, cslot, lane, gc);
-      } else {
-        fill_sentinel<Q, SPT>(d);
-        message_adjoint<Q, SPT, SOFT, false>(cf, a, d, g, acc, gc);
+      }
+    }
+    __syncthreads();  // the table is written by lanes < Q, read by all
+  }
+
+  const cptr<int> prog = as_const(reinterpret_cast<const int*>(A.steps)) + (size_t)tree * A.n_int * 4;
+  const uint32_t treebytes = (uint32_t)((size_t)A.n_int * Q * L * 4);
+  const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * A.n_int * Q * L, treebytes);
+  // inactive lanes address past the buffer: stores drop, loads return 0
+  const int voff = active ? site * 4 : 0x7FFFFFF0;
+  const int rowbytes = L * 4;
+
+  float dv[Q][SPT];
+  if constexpr (FWD) {
+    I4 nxt = load_step(prog, 0);
+    for (int k = 0; k < A.n_int; ++k) {
+      const I4 stp = nxt;
+      if (k + 1 < A.n_int) nxt = load_step(prog, k + 1);
+      // gather both children (LDS reads in flight together)
+      float d[2][Q][SPT];
+      int code[2][SPT];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? stp.y : stp.z;
+        const int kind = (desc >> 24) & 3;
+        if (kind == kKindLeaf) {
+          ld_codes<SPT>(lleaf + ((desc & 0xFFFF) * kWave + lane) * SPT, code[c]);
+          if constexpr (LFAST) {
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+              float r[Q];
+              lds_vec_get<Q>(tab + code[c][s] * Q, r);
+#pragma unroll
+              for (int i = 0; i < Q; ++i) d[c][i][s] = r[i];  // already the message
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < Q; ++j)
+#pragma unroll
+              for (int s = 0; s < SPT; ++s)
+                d[c][j][s] = (code[c][s] == j) ? 0.0f : kSentinel;
+          }
+        } else {
+          lds_get<Q, SPT>(slots, kind == kKindInt ? ((desc >> 16) & 0xFF) : kSentSlot, lane, d[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? stp.y : stp.z;
+        float m[Q][SPT];
+        if (LFAST && ((desc >> 24) & 3) == kKindLeaf) {
+#pragma unroll
+          for (int i = 0; i < Q; ++i)
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) m[i][s] = d[c][i][s];
+        } else {
+          message<Q, SPT, MODE>(cf, a, bcoef, d[c], m);
+        }
+#pragma unroll
+        for (int i = 0; i < Q; ++i)
+#pragma unroll
+          for (int s = 0; s < SPT; ++s) dv[i][s] = (c == 0) ? m[i][s] : dv[i][s] + m[i][s];
+      }
+      const int row = stp.x & 0xFFFF;
+      const int oslot = (stp.x >> 16) & 0xFF;
+#pragma unroll
+      for (int i = 0; i < Q; ++i) bst<SPT>(rdp, voff, (row * Q + i) * rowbytes, dv[i]);
+      if (oslot != 0xFF) lds_put<Q, SPT>(slots, oslot, lane, dv);
+    }
+  } else {
+    // adjoint only: the root row comes from the table
+#pragma unroll
+    for (int i = 0; i < Q; ++i) bld<SPT>(rdp, voff, ((A.n_int - 1) * Q + i) * rowbytes, dv[i]);
+  }
+
+  // ---- root: score + cotangent ----
+  float score[SPT], groot[Q][SPT];
+  root_score<Q, SPT, SOFT>(dv, a, bcoef, A.hard_root != 0, score, groot);
+  double tot = 0.0;
+  if constexpr (FWD) {
+    if (active) {
+#pragma unroll
+      for (int s = 0; s < SPT; ++s) tot += (double)score[s];
+      if (A.site_score) st<SPT>(A.site_score + (size_t)tree * L + site, score);
+    }
+    tot = wave_sum(tot);
+  }
+
+  // acc: dC accumulators (in the factored form x K[i][j] at the end; leaf
+  // one-hot contributions are pre-divided by K via the IK table)
+  float acc[Q][Q];
+  if constexpr (BWD) {
+    const float dscale = A.dts ? as_const(A.dts)[tree] : 1.0f;
+    const float f = active ? dscale : 0.0f;
+#pragma unroll
+    for (int i = 0; i < Q; ++i)
+#pragma unroll
+      for (int s = 0; s < SPT; ++s) groot[i][s] *= f;
+#pragma unroll
+    for (int i = 0; i < Q; ++i)
+#pragma unroll
+      for (int j = 0; j < Q; ++j) acc[i][j] = 0.0f;
+    const bool want_marg = A.marg != nullptr;
+    const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * A.n_int * Q * L : A.dp,
+                                 treebytes);
+    int8_t* at = A.anc ? A.anc + (size_t)tree * A.n_int * L + sc : nullptr;
+
+    // software pipeline: DP rows of the next step's internal children in flight
+    float nd[2][Q][SPT];
+    I4 nstp = load_step(prog, A.n_int - 1);
+    auto prefetch = [&](const I4& s2) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? s2.y : s2.z;
+        if (((desc >> 24) & 3) == kKindInt) {
+          const int crow = desc & 0xFFFF;
+#pragma unroll
+          for (int j = 0; j < Q; ++j) bld<SPT>(rdp, voff, (crow * Q + j) * rowbytes, nd[c][j]);
+        }
+      }
+    };
+    lds_put<Q, SPT>(slots, kRootSlot, lane, groot);
+    prefetch(nstp);
+    for (int k = A.n_int - 1; k >= 0; --k) {
+      const I4 stp = nstp;
+      float cd[2][Q][SPT];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < Q; ++j)
+#pragma unroll
+          for (int s = 0; s < SPT; ++s) cd[c][j][s] = nd[c][j][s];
+      if (k > 0) {
+        nstp = load_step(prog, k - 1);
+        prefetch(nstp);
+      }
+      if (stp.w & kStepUnreached) continue;
+      const int row = stp.x & 0xFFFF;
+      float g[Q][SPT];
+      lds_get<Q, SPT>(slots, (stp.w & kStepRoot) ? kRootSlot : ((stp.x >> 16) & 0xFF), lane, g);
+      int code[2][SPT];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? stp.y : stp.z;
+        const int kind = (desc >> 24) & 3;
+        if (kind == kKindLeaf) {
+          ld_codes<SPT>(lleaf + ((desc & 0xFFFF) * kWave + lane) * SPT, code[c]);
+        } else if (kind != kKindInt) {
+          lds_get<Q, SPT>(slots, kSentSlot, lane, cd[c]);
+        }
+      }
+      if (want_marg) {
+#pragma unroll
+        for (int i = 0; i < Q; ++i) bst<SPT>(rmg, voff, (row * Q + i) * rowbytes, g[i]);
+      }
+      if (at && active) {
+        int best[SPT];
+#pragma unroll
+        for (int s = 0; s < SPT; ++s) {
+          float bv = g[0][s];
+          int bi = 0;
+#pragma unroll
+          for (int i = 1; i < Q; ++i)
+            if (g[i][s] > bv) { bv = g[i][s]; bi = i; }
+          best[s] = bi;
+        }
+        st_codes<SPT>(at + (size_t)row * L, best);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? stp.y : stp.z;
+        const int kind = (desc >> 24) & 3;
+        bool onehot = false;
+        if (kind == kKindLeaf) {
+          if constexpr (LFAST) {
+            bool miss = false;
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) miss |= code[c][s] == Q;
+            onehot = !__any(miss);
+          }
+          if (!onehot) {
+#pragma unroll
+            for (int j = 0; j < Q; ++j)
+#pragma unroll
+              for (int s = 0; s < SPT; ++s)
+                cd[c][j][s] = (code[c][s] == j) ? 0.0f : kSentinel;
+          }
+        }
+        if (onehot) {
+          // exact leaf weights are one-hot: dC[i][code] += g_i
+#pragma unroll
+          for (int s = 0; s < SPT; ++s) {
+            float oh[Q], t[Q];
+#pragma unroll
+            for (int j = 0; j < Q; ++j) oh[j] = (code[c][s] == j) ? 1.0f : 0.0f;
+            if constexpr (MODE == kSoftK) {
+              float ik[Q];
+              lds_vec_get<Q>(tab + 32 + code[c][s] * Q, ik);
+#pragma unroll
+              for (int i = 0; i < Q; ++i) t[i] = g[i][s] * ik[i];
+            } else {
+#pragma unroll
+              for (int i = 0; i < Q; ++i) t[i] = g[i][s];
+            }
+#pragma unroll
+            for (int i = 0; i < Q; ++i)
+#pragma unroll
+              for (int j = 0; j < Q; ++j) acc[i][j] = fmaf(t[i], oh[j], acc[i][j]);
+          }
+        } else {
+          float gc[Q][SPT];
+          message_adjoint<Q, SPT, MODE>(cf, a, cd[c], g, acc, gc);
+          if (kind == kKindInt) {
+            const int cslot = (desc >> 16) & 0xFF;
+            if (desc & kStepAccumulate) {
+              float old[Q][SPT];
+              lds_get<Q, SPT>(slots, cslot, lane, old);
+#pragma unroll
+              for (int j = 0; j < Q; ++j)
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) gc[j][s] += old[j][s];
+            }
+            lds_put<Q, SPT>(slots, cslot, lane, gc);
+          }
+        }
       }
     }
   }
-  double* out = part + (size_t)blockIdx.x * Q * Q;
+
+  // ---- epilogue: deterministic two-level reduction, last block finishes ----
+  const int nb = A.B * A.tiles;
+  double dsum[Q * Q];
+  if constexpr (BWD) {
 #pragma unroll
-  for (int i = 0; i < Q; ++i)
+    for (int i = 0; i < Q; ++i)
 #pragma unroll
-    for (int j = 0; j < Q; ++j) {
-      const double v = wave_sum((double)acc[i][j]);
-      if (lane == 0) out[i * Q + j] = v;
+      for (int j = 0; j < Q; ++j) {
+        double v = (double)acc[i][j];
+        if constexpr (MODE == kSoftK) v = v * (double)cf.k[i][j];
+        dsum[i * Q + j] = wave_sum(v);
+      }
+  }
+  if (lane == 0) {
+    if (FWD) store_sc1(A.part_tree + blockIdx.x, tot);
+    if (BWD) {
+#pragma unroll
+      for (int q = 0; q < Q * Q; ++q) store_sc1(A.part_dc + (size_t)q * nb + blockIdx.x, dsum[q]);
     }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0)
+    old = __hip_atomic_fetch_add(A.counters + tree, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, kWave);
+  if (old != A.tiles - 1) return;
+  // last tile of this tree
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (lane == 0) __hip_atomic_store(A.counters + tree, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const size_t t0 = (size_t)tree * A.tiles;
+  if constexpr (FWD) {
+    const double s = wave_sum_strided(A.part_tree + t0, A.tiles, lane);
+    if (lane == 0) A.tree_score[tree] = (float)s;
+  }
+  if constexpr (BWD) {
+    for (int q = 0; q < Q * Q; ++q) {
+      const double s = wave_sum_strided(A.part_dc + (size_t)q * nb + t0, A.tiles, lane);
+      if (lane == 0) store_sc1(A.tree_dc + (size_t)q * A.B + tree, s);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old2 = 0;
+    if (lane == 0)
+      old2 = __hip_atomic_fetch_add(A.counters + A.B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old2 = __shfl(old2, 0, kWave);
+    if (old2 != A.B - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (lane == 0) __hip_atomic_store(A.counters + A.B, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = 0; q < Q * Q; ++q) {
+      const double s = wave_sum_strided(A.tree_dc + (size_t)q * A.B, A.B, lane);
+      if (lane == 0) A.d_cost[q] = (float)s;
+    }
+  }
+}
+
+template <int Q, int SPT, int MODE, int PHASE>
+__device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds) {
+  // leaf messages have the closed form C[i][code] when the 1e5 sentinel
+  // dominates (hard: range(C) < 1e5; soft: exp(-(1e5 - range)/tau) < 2^-64)
+  float cmin, cmax;
+  cost_range<Q>(A.cost, cmin, cmax);
+  const float range = cmax - cmin;
+  const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
+  if (lfast)
+    sankoff_body<Q, SPT, MODE, PHASE, true>(A, lds);
+  else
+    sankoff_body<Q, SPT, MODE, PHASE, false>(A, lds);
+}
+
+template <int Q, int SPT, bool SOFT, int PHASE>
+__global__ __launch_bounds__(kWave) void sankoff_kernel(KArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if constexpr (!SOFT) {
+    sankoff_dispatch_leaf<Q, SPT, kHard, PHASE>(A, lds);
+  } else {
+    float cmin, cmax;
+    cost_range<Q>(A.cost, cmin, cmax);
+    if (use_ktrick(cmin, cmax, A.a))
+      sankoff_dispatch_leaf<Q, SPT, kSoftK, PHASE>(A, lds);
+    else
+      sankoff_dispatch_leaf<Q, SPT, kSoftDirect, PHASE>(A, lds);
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -542,13 +904,13 @@ __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
 #pragma unroll
   for (int i = 0; i < Q; ++i)
 #pragma unroll
-    for (int j = 0; j < Q; ++j) c[i][j] = uniform(cost[i * Q + j]);
-  const int2* prog = bt + (size_t)tree * n_int;
+    for (int j = 0; j < Q; ++j) c[i][j] = as_const(cost)[i * Q + j];
+  const cptr<int> prog = as_const(reinterpret_cast<const int*>(bt)) + (size_t)tree * n_int * 2;
   const size_t rowstride = (size_t)Q * L;
   const float* dpt = dp + (size_t)tree * n_int * rowstride + site;
   int8_t* at = anc + (size_t)tree * n_int * L + site;
   for (int k = 0; k < n_int; ++k) {
-    const int2 e = prog[k];
+    const int2 e = make_int2(prog[2 * k], prog[2 * k + 1]);
     const int x = e.x & 0xFFFF;
     const int kind = (e.x >> 16) & 0xF;
     int out[SPT];
@@ -601,49 +963,6 @@ __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
   }
 }
 
-// --------------------------------------------------------------------------
-// reductions (fixed order => bitwise reproducible)
-// --------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void reduce_tree_kernel(const double* __restrict__ part,
-                                                         int tiles, float* __restrict__ out) {
-  __shared__ double sh[256];
-  const int tree = blockIdx.x;
-  double v = 0.0;
-  for (int t = threadIdx.x; t < tiles; t += 256) v += part[(size_t)tree * tiles + t];
-  sh[threadIdx.x] = v;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[tree] = (float)sh[0];
-}
-
-template <int Q>
-__global__ __launch_bounds__(256) void reduce_dcost_kernel(const double* __restrict__ part,
-                                                          int nblocks, const float* __restrict__ cost,
-                                                          float a, int soft, float* __restrict__ out) {
-  __shared__ double sh[256];
-  const int q = blockIdx.x;
-  double v = 0.0;
-  for (int t = threadIdx.x; t < nblocks; t += 256) v += part[(size_t)t * Q * Q + q];
-  sh[threadIdx.x] = v;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    double f = 1.0;
-    if (soft) {
-      Coef<Q> cf;
-      load_coef<Q, true>(cost, a, cf);
-      if (cf.ktrick) f = (double)cf.k[q / Q][q % Q];
-    }
-    out[q] = (float)(sh[0] * f);
-  }
-}
-
 // dp [B][n_int][Q][L] -> trex VmappedDPTable [B][L][n_all][Q]
 __global__ __launch_bounds__(256) void to_trex_layout_kernel(const float* __restrict__ dp,
                                                             const int8_t* __restrict__ leaves,
@@ -689,23 +1008,25 @@ int check_shape(const char* fn, int B, int L, int n_all, int Q, Shape* sh) {
   return TREX_OK;
 }
 
-// sites per lane: widest that divides L and keeps the LDS stack <= 10 KiB per
-// wave (>= 16 resident waves per CU); TREX_SPT overrides for tuning.
-int pick_spt(int L, int n_slots, int Q) {
-  static int forced = [] {
+int tiles_for(int L, int spt) { return (L + kWave * spt - 1) / (kWave * spt); }
+
+size_t lds_bytes(int n_slots, int nl, int Q, int spt) {
+  const size_t b = (size_t)kTabFloats * 4 + (size_t)(n_slots + 2) * Q * kWave * spt * 4 +
+                   (size_t)nl * kWave * spt;
+  return (b + 15) & ~(size_t)15;
+}
+
+// sites per lane: 2 when L is even and the wave's LDS (stack + leaf tile)
+// stays <= 12 KiB, else 1.  TREX_SPT=1|2 overrides (tuning).
+int pick_spt(int L, int n_slots, int nl, int Q) {
+  static const int forced = [] {
     const char* e = std::getenv("TREX_SPT");
     return e ? std::atoi(e) : 0;
   }();
-  if (forced == 1 || forced == 2 || forced == 4) {
-    if (L % forced == 0) return forced;
-  }
-  for (int s : {4, 2}) {
-    if (L % s == 0 && (size_t)n_slots * Q * kWave * s * 4 <= 10240) return s;
-  }
+  if ((forced == 1 || forced == 2) && L % forced == 0) return forced;
+  if (L % 2 == 0 && lds_bytes(n_slots, nl, Q, 2) <= 12288) return 2;
   return 1;
 }
-
-int tiles_for(int L, int spt) { return (L + kWave * spt - 1) / (kWave * spt); }
 
 int hip_check(const char* fn) {
   const hipError_t e = hipGetLastError();
@@ -713,51 +1034,7 @@ int hip_check(const char* fn) {
   return TREX_OK;
 }
 
-template <int Q, int SPT, bool SOFT>
-void launch_fwd(const Shape& s, int tiles, size_t lds, hipStream_t st, const int4* steps,
-                const int8_t* leaves, const float* cost, float a, float bcoef, int hard_root,
-                float* dp, float* site_score, double* part) {
-  hipLaunchKernelGGL((sankoff_fwd_kernel<Q, SPT, SOFT>), dim3(s.B * tiles), dim3(kWave), lds, st,
-                     steps, leaves, cost, s.ni, s.nl, s.L, tiles, a, bcoef, hard_root, dp,
-                     site_score, part);
-}
-
-template <int Q, int SPT, bool SOFT>
-void launch_bwd(const Shape& s, int tiles, size_t lds, hipStream_t st, const int4* steps,
-                const int8_t* leaves, const float* cost, float a, float bcoef, int hard_root,
-                const float* dp, const float* dts, float* marg, int8_t* anc, double* part) {
-  hipLaunchKernelGGL((sankoff_bwd_kernel<Q, SPT, SOFT>), dim3(s.B * tiles), dim3(kWave), lds, st,
-                     steps, leaves, cost, s.ni, s.nl, s.L, tiles, a, bcoef, hard_root, dp, dts,
-                     marg, anc, part);
-}
-
-template <int Q, bool SOFT>
-void dispatch_fwd(int spt, const Shape& s, int tiles, size_t lds, hipStream_t st,
-                  const int4* steps, const int8_t* leaves, const float* cost, float a, float bcoef,
-                  int hr, float* dp, float* ss, double* part) {
-  if (spt == 4)
-    launch_fwd<Q, 4, SOFT>(s, tiles, lds, st, steps, leaves, cost, a, bcoef, hr, dp, ss, part);
-  else if (spt == 2)
-    launch_fwd<Q, 2, SOFT>(s, tiles, lds, st, steps, leaves, cost, a, bcoef, hr, dp, ss, part);
-  else
-    launch_fwd<Q, 1, SOFT>(s, tiles, lds, st, steps, leaves, cost, a, bcoef, hr, dp, ss, part);
-}
-
-template <int Q, bool SOFT>
-void dispatch_bwd(int spt, const Shape& s, int tiles, size_t lds, hipStream_t st,
-                  const int4* steps, const int8_t* leaves, const float* cost, float a, float bcoef,
-                  int hr, const float* dp, const float* dts, float* marg, int8_t* anc,
-                  double* part) {
-  if (spt == 4)
-    launch_bwd<Q, 4, SOFT>(s, tiles, lds, st, steps, leaves, cost, a, bcoef, hr, dp, dts, marg,
-                           anc, part);
-  else if (spt == 2)
-    launch_bwd<Q, 2, SOFT>(s, tiles, lds, st, steps, leaves, cost, a, bcoef, hr, dp, dts, marg,
-                           anc, part);
-  else
-    launch_bwd<Q, 1, SOFT>(s, tiles, lds, st, steps, leaves, cost, a, bcoef, hr, dp, dts, marg,
-                           anc, part);
-}
+int64_t counters_bytes(int B) { return ((int64_t)4 * (B + 1) + 255) / 256 * 256; }
 
 void tau_coefs(float tau, float* a, float* bcoef) {
   if (tau > 0.0f) {
@@ -769,6 +1046,34 @@ void tau_coefs(float tau, float* a, float* bcoef) {
   }
 }
 
+template <int Q, int SPT, bool SOFT>
+void launch_phase(int phase, int grid, size_t lds, hipStream_t st, const KArgs& A) {
+  if (phase == 1)
+    hipLaunchKernelGGL((sankoff_kernel<Q, SPT, SOFT, 1>), dim3(grid), dim3(kWave), lds, st, A);
+  else if (phase == 2)
+    hipLaunchKernelGGL((sankoff_kernel<Q, SPT, SOFT, 2>), dim3(grid), dim3(kWave), lds, st, A);
+  else
+    hipLaunchKernelGGL((sankoff_kernel<Q, SPT, SOFT, 3>), dim3(grid), dim3(kWave), lds, st, A);
+}
+
+template <int Q>
+void dispatch_q(int phase, int spt, bool soft, int grid, size_t lds, hipStream_t st,
+                const KArgs& A) {
+  if (spt == 2) {
+    if (soft) launch_phase<Q, 2, true>(phase, grid, lds, st, A);
+    else launch_phase<Q, 2, false>(phase, grid, lds, st, A);
+  } else {
+    if (soft) launch_phase<Q, 1, true>(phase, grid, lds, st, A);
+    else launch_phase<Q, 1, false>(phase, grid, lds, st, A);
+  }
+}
+
+// common entry: validates, fills KArgs, launches one phase
+int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const int8_t* leaves,
+              const float* cost, int B, int L, int n_all, int Q, float tau, unsigned flags,
+              float* dp, float* site_score, float* tree_score, const float* dts, float* d_cost,
+              float* marg, int8_t* anc, void* workspace, int64_t workspace_bytes, void* stream);
+
 }  // namespace
 
 int set_error(int code, const char* fmt, ...) {
@@ -779,60 +1084,102 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
+namespace {
+
+int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const int8_t* leaves,
+              const float* cost, int B, int L, int n_all, int Q, float tau, unsigned flags,
+              float* dp, float* site_score, float* tree_score, const float* dts, float* d_cost,
+              float* marg, int8_t* anc, void* workspace, int64_t workspace_bytes, void* stream) {
+  Shape s;
+  if (int e = check_shape(fn, B, L, n_all, Q, &s)) return e;
+  if (!plan || !leaves || !cost || !workspace)
+    return set_error(TREX_E_ARG, "%s: null pointer argument", fn);
+  if ((phase & 1) && !tree_score) return set_error(TREX_E_ARG, "%s: tree_score is required", fn);
+  if ((phase & 2) && (!dp || !d_cost))
+    return set_error(TREX_E_ARG, "%s: dp and d_cost are required", fn);
+  if (!(tau >= 0.0f) || std::isinf(tau))
+    return set_error(TREX_E_ARG, "%s: tau must be finite and >= 0 (got %g)", fn, tau);
+  if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
+    return set_error(TREX_E_ARG, "%s: workspace too small", fn);
+  if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  const int spt = pick_spt(L, n_slots, s.nl, Q);
+  const int tiles = tiles_for(L, spt);
+  const size_t lds = lds_bytes(n_slots, s.nl, Q, spt);
+  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
+  if ((int64_t)B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
+  KArgs A;
+  A.steps = reinterpret_cast<const int4*>(plan + TREX_PLAN_HEADER_INTS);
+  A.leaves = leaves;
+  A.cost = cost;
+  A.n_int = s.ni;
+  A.nl = s.nl;
+  A.L = L;
+  A.tiles = tiles;
+  A.B = B;
+  A.n_slots = n_slots;
+  tau_coefs(tau, &A.a, &A.bcoef);
+  A.hard_root = (flags & TREX_FLAG_HARD_ROOT) ? 1 : 0;
+  A.dp = dp;
+  A.site_score = site_score;
+  A.tree_score = tree_score;
+  A.dts = dts;
+  A.marg = marg;
+  A.anc = anc;
+  A.d_cost = d_cost;
+  char* w = static_cast<char*>(workspace);
+  const int64_t nbmax = (int64_t)B * tiles_for(L, 1);
+  A.counters = reinterpret_cast<int*>(w);
+  w += counters_bytes(B);
+  A.part_tree = reinterpret_cast<double*>(w);
+  w += nbmax * 8;
+  A.part_dc = reinterpret_cast<double*>(w);
+  w += nbmax * 8 * Q * Q;
+  A.tree_dc = reinterpret_cast<double*>(w);
+  const bool soft = tau > 0.0f;
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = B * tiles;
+  switch (Q) {
+    case 2: dispatch_q<2>(phase, spt, soft, grid, lds, st, A); break;
+    case 3: dispatch_q<3>(phase, spt, soft, grid, lds, st, A); break;
+    case 4: dispatch_q<4>(phase, spt, soft, grid, lds, st, A); break;
+  }
+  return hip_check(fn);
+}
+
+}  // namespace
+
 }  // namespace trex
 
 using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 1; }
+extern "C" int trex_version(void) { return 2; }
 
 extern "C" int64_t trex_workspace_bytes(int B, int L, int n_all, int Q) {
   if (B <= 0 || L <= 0 || Q <= 0) return 0;
   const int64_t nb = (int64_t)B * tiles_for(L, 1);
-  return 256 + nb * 8 + nb * (int64_t)Q * Q * 8;
+  return counters_bytes(B) + nb * 8 * (1 + (int64_t)Q * Q) + (int64_t)Q * Q * B * 8 + 256;
+}
+
+extern "C" int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!workspace || workspace_bytes <= 0)
+    return set_error(TREX_E_ARG, "trex_workspace_init: bad arguments");
+  if (hipMemsetAsync(workspace, 0, (size_t)workspace_bytes, (hipStream_t)stream) != hipSuccess)
+    return hip_check("trex_workspace_init");
+  return hip_check("trex_workspace_init");
 }
 
 extern "C" int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
                                 const float* cost, int B, int L, int n_all, int Q, float tau,
                                 unsigned flags, float* dp, float* site_score, float* tree_score,
                                 void* workspace, int64_t workspace_bytes, void* stream) {
-  Shape s;
-  if (int e = check_shape("trex_sankoff_fwd", B, L, n_all, Q, &s)) return e;
-  if (!plan || !leaves || !cost || !tree_score || !workspace)
-    return set_error(TREX_E_ARG, "trex_sankoff_fwd: null pointer argument");
-  if (!(tau >= 0.0f) || std::isinf(tau))
-    return set_error(TREX_E_ARG, "trex_sankoff_fwd: tau must be finite and >= 0 (got %g)", tau);
-  if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
-    return set_error(TREX_E_ARG, "trex_sankoff_fwd: workspace too small");
-  if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "trex_sankoff_fwd: bad n_slots");
-  const int spt = pick_spt(L, n_slots, Q);
-  const int tiles = tiles_for(L, spt);
-  const size_t lds = (size_t)std::max(n_slots, 1) * Q * kWave * spt * sizeof(float);
-  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "trex_sankoff_fwd: LDS stack too deep");
-  hipStream_t st = (hipStream_t)stream;
-  const int4* steps = reinterpret_cast<const int4*>(plan + TREX_PLAN_HEADER_INTS);
-  double* part = reinterpret_cast<double*>(workspace);
-  float a, bc;
-  tau_coefs(tau, &a, &bc);
-  const int hr = (flags & TREX_FLAG_HARD_ROOT) ? 1 : 0;
-  const bool soft = tau > 0.0f;
-#define TREX_FWD(QQ)                                                                         \
-  if (soft)                                                                                  \
-    dispatch_fwd<QQ, true>(spt, s, tiles, lds, st, steps, leaves, cost, a, bc, hr, dp,       \
-                           site_score, part);                                                \
-  else                                                                                       \
-    dispatch_fwd<QQ, false>(spt, s, tiles, lds, st, steps, leaves, cost, a, bc, hr, dp,      \
-                            site_score, part);
-  switch (Q) {
-    case 2: TREX_FWD(2) break;
-    case 3: TREX_FWD(3) break;
-    case 4: TREX_FWD(4) break;
-  }
-#undef TREX_FWD
-  if (int e = hip_check("trex_sankoff_fwd")) return e;
-  hipLaunchKernelGGL(reduce_tree_kernel, dim3(B), dim3(256), 0, st, part, tiles, tree_score);
-  return hip_check("trex_sankoff_fwd(reduce)");
+  if (!dp)
+    return set_error(TREX_E_UNSUPPORTED,
+                     "trex_sankoff_fwd: dp is required (the reference returns the table)");
+  return run_phase("trex_sankoff_fwd", 1, plan, n_slots, leaves, cost, B, L, n_all, Q, tau, flags,
+                   dp, site_score, tree_score, nullptr, nullptr, nullptr, nullptr, workspace,
+                   workspace_bytes, stream);
 }
 
 extern "C" int trex_sankoff_bwd(const int32_t* plan, int n_slots, const int8_t* leaves,
@@ -840,43 +1187,20 @@ extern "C" int trex_sankoff_bwd(const int32_t* plan, int n_slots, const int8_t* 
                                 unsigned flags, const float* dp, const float* d_tree_score,
                                 float* d_cost, float* marginals, int8_t* anc_states,
                                 void* workspace, int64_t workspace_bytes, void* stream) {
-  Shape s;
-  if (int e = check_shape("trex_sankoff_bwd", B, L, n_all, Q, &s)) return e;
-  if (!plan || !leaves || !cost || !dp || !d_cost || !workspace)
-    return set_error(TREX_E_ARG, "trex_sankoff_bwd: null pointer argument");
-  if (!(tau >= 0.0f) || std::isinf(tau))
-    return set_error(TREX_E_ARG, "trex_sankoff_bwd: tau must be finite and >= 0 (got %g)", tau);
-  if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
-    return set_error(TREX_E_ARG, "trex_sankoff_bwd: workspace too small");
-  if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "trex_sankoff_bwd: bad n_slots");
-  const int spt = pick_spt(L, n_slots, Q);
-  const int tiles = tiles_for(L, spt);
-  const size_t lds = (size_t)std::max(n_slots, 1) * Q * kWave * spt * sizeof(float);
-  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "trex_sankoff_bwd: LDS stack too deep");
-  hipStream_t st = (hipStream_t)stream;
-  const int4* steps = reinterpret_cast<const int4*>(plan + TREX_PLAN_HEADER_INTS);
-  double* part = reinterpret_cast<double*>(static_cast<char*>(workspace) + 256 +
-                                           (int64_t)B * tiles_for(L, 1) * 8);
-  float a, bc;
-  tau_coefs(tau, &a, &bc);
-  const int hr = (flags & TREX_FLAG_HARD_ROOT) ? 1 : 0;
-  const bool soft = tau > 0.0f;
-#define TREX_BWD(QQ)                                                                         \
-  if (soft)                                                                                  \
-    dispatch_bwd<QQ, true>(spt, s, tiles, lds, st, steps, leaves, cost, a, bc, hr, dp,       \
-                           d_tree_score, marginals, anc_states, part);                       \
-  else                                                                                       \
-    dispatch_bwd<QQ, false>(spt, s, tiles, lds, st, steps, leaves, cost, a, bc, hr, dp,      \
-                            d_tree_score, marginals, anc_states, part);                      \
-  hipLaunchKernelGGL(reduce_dcost_kernel<QQ>, dim3(QQ * QQ), dim3(256), 0, st, part,           \
-                     B * tiles, cost, a, soft ? 1 : 0, d_cost);
-  switch (Q) {
-    case 2: TREX_BWD(2) break;
-    case 3: TREX_BWD(3) break;
-    case 4: TREX_BWD(4) break;
-  }
-#undef TREX_BWD
-  return hip_check("trex_sankoff_bwd");
+  return run_phase("trex_sankoff_bwd", 2, plan, n_slots, leaves, cost, B, L, n_all, Q, tau, flags,
+                   const_cast<float*>(dp), nullptr, nullptr, d_tree_score, d_cost, marginals,
+                   anc_states, workspace, workspace_bytes, stream);
+}
+
+extern "C" int trex_sankoff_fwd_bwd(const int32_t* plan, int n_slots, const int8_t* leaves,
+                                    const float* cost, int B, int L, int n_all, int Q, float tau,
+                                    unsigned flags, float* dp, float* site_score,
+                                    float* tree_score, const float* d_tree_score, float* d_cost,
+                                    float* marginals, int8_t* anc_states, void* workspace,
+                                    int64_t workspace_bytes, void* stream) {
+  return run_phase("trex_sankoff_fwd_bwd", 3, plan, n_slots, leaves, cost, B, L, n_all, Q, tau,
+                   flags, dp, site_score, tree_score, d_tree_score, d_cost, marginals, anc_states,
+                   workspace, workspace_bytes, stream);
 }
 
 extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, const float* cost,
@@ -913,13 +1237,12 @@ extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, con
 
 extern "C" int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,
                                       int n_all, int Q, float* out, void* stream) {
-  Shape s;
   if (B <= 0 || L <= 0 || n_all < 3 || Q < 2 || !dp || !leaves || !out)
     return set_error(TREX_E_ARG, "trex_dp_to_trex_layout: bad arguments");
-  s.nl = (n_all + 1) / 2;
+  const int nl = (n_all + 1) / 2;
   const size_t total = (size_t)B * n_all * L;
   const int grid = (int)std::min<size_t>((total + 255) / 256, 65536);
   hipLaunchKernelGGL(to_trex_layout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dp,
-                     leaves, B, L, n_all, s.nl, Q, out);
+                     leaves, B, L, n_all, nl, Q, out);
   return hip_check("trex_dp_to_trex_layout");
 }

@@ -77,6 +77,8 @@ class SankoffEngine:
         if nbytes <= 0:
             raise ValueError("bad shape for workspace")
         self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        # arrival counters of the in-kernel reductions start at zero
+        check(lib().trex_workspace_init(ptr(self.workspace), nbytes, stream_handle(self.device)))
 
     # -- shapes ------------------------------------------------------------
     @property
@@ -103,13 +105,14 @@ class SankoffEngine:
         self._check_inputs(leaves, cost)
         p = self.plan
         o = out or {}
-        dp_t = None
         if dp is True:
             dp_t = o.get("dp")
             if dp_t is None:
                 dp_t = torch.empty(self.dp_shape, dtype=torch.float32, device=self.device)
         elif dp is not False and dp is not None:
             dp_t = dp
+        else:
+            raise ValueError("forward writes the DP table (trex returns it); pass dp=True")
         ss = None
         if site_score:
             ss = o.get("site_score")
@@ -157,6 +160,44 @@ class SankoffEngine:
             ptr(self.workspace), self.workspace.numel(), stream_handle(self.device)))
         return dc, mg, an
 
+    def fwd_bwd(self, leaves, cost, tau: float = 0.0, d_tree_score=None, *, site_score=False,
+                marginals=False, anc_states=False, hard_root=False, out=None):
+        """Fused forward + adjoint in one launch (trex_sankoff_fwd_bwd).
+
+        Returns (ForwardResult, d_cost, marginals | None, anc_states | None).
+        """
+        torch = _torch()
+        self._check_inputs(leaves, cost)
+        p = self.plan
+        o = out or {}
+
+        def buf(key, shape, dtype, want=True):
+            if not want:
+                return None
+            t = o.get(key)
+            if t is None:
+                t = torch.empty(shape, dtype=dtype, device=self.device)
+            return t
+
+        dp_t = buf("dp", self.dp_shape, torch.float32)
+        ss = buf("site_score", (p.B, self.L), torch.float32, site_score)
+        ts = buf("tree_score", (p.B,), torch.float32)
+        dc = buf("d_cost", (self.Q, self.Q), torch.float32)
+        mg = buf("marginals", self.dp_shape, torch.float32, marginals)
+        an = buf("anc_states", (p.B, p.n_int, self.L), torch.int8, anc_states)
+        if d_tree_score is not None:
+            d_tree_score = torch.as_tensor(d_tree_score, dtype=torch.float32,
+                                           device=self.device).contiguous()
+            if d_tree_score.shape != (p.B,):
+                raise ValueError("d_tree_score must be (B,)")
+        flags = TREX_FLAG_HARD_ROOT if hard_root else 0
+        check(lib().trex_sankoff_fwd_bwd(
+            ptr(self.plan_dev), p.n_slots, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
+            self.Q, float(tau), flags, ptr(dp_t), ptr(ss), ptr(ts), ptr(d_tree_score), ptr(dc),
+            ptr(mg), ptr(an), ptr(self.workspace), self.workspace.numel(),
+            stream_handle(self.device)))
+        return ForwardResult(ts, dp_t, ss), dc, mg, an
+
     def backtrack(self, cost, dp):
         """trex-exact ancestral states (B, n_int, L) int8 (sankoff.py:166-185)."""
         torch = _torch()
@@ -169,9 +210,8 @@ class SankoffEngine:
 
     def value_and_grad(self, leaves, cost, tau: float = 0.0, d_tree_score=None,
                        hard_root=False):
-        """(tree_score (B,), d_cost (Q, Q)) -- one fwd + one adjoint sweep."""
-        f = self.forward(leaves, cost, tau, dp=True, hard_root=hard_root)
-        dc, _, _ = self.backward(leaves, cost, tau, f.dp, d_tree_score, hard_root=hard_root)
+        """(tree_score (B,), d_cost (Q, Q)) -- fused fwd + adjoint launch."""
+        f, dc, _, _ = self.fwd_bwd(leaves, cost, tau, d_tree_score, hard_root=hard_root)
         return f.tree_score, dc
 
     def to_trex_layout(self, dp, leaves):
