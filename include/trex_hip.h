@@ -146,6 +146,66 @@ int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, const float* c
 int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,
                            int n_all, int Q, float* out, void* stream);
 
+/* ========================================================================
+ * Tree-cost path (src/trex/tree.py).  N = n_nodes, S = soft sequences
+ * [N][L][Q] (flattened K = L*Q per node), A = adjacency [N][N] with
+ * A[i][j] = "i is a child of j" (src/trex/utils/types.py:30-35).
+ * ====================================================================== */
+
+/* discretize_tree_topology (tree.py:31-47): out[i] = one_hot(argmax A[i]) */
+int trex_tree_discretize(const float* A, int nrows, int ncols, int n_nodes, float* out,
+                         void* stream);
+
+/* update_seq (tree.py:110-130): S_anc[a][l] = softmax_q(T * X[a][l][q]),
+ * written into rows n_leaf.. of S; and its VJP (dX = T S (dS - <S, dS>)). */
+int trex_tree_update_seq(const float* x, int n_anc, int L, int Q, float temperature,
+                         float* s_anc, void* stream);
+int trex_tree_update_seq_bwd(const float* s_anc, const float* ds_anc, int n_anc, int L, int Q,
+                             float temperature, float* dx, void* stream);
+
+/* update_tree (tree.py:50-107) with explicit Gumbel noise (the reference's
+ * jax.random.gumbel draw, :71): theta/noise/gates [N-1][n_anc] (noise,
+ * gates may be NULL); A [N][N] = row softmax of the masked logits; VJP. */
+int trex_tree_update_tree(const float* theta, const float* noise, const float* gates, int N,
+                          int n_anc, float temperature, float* A, void* stream);
+int trex_tree_update_tree_bwd(const float* A, const float* dA, const float* gates, int N,
+                              int n_anc, float temperature, float* dtheta, void* stream);
+
+/* Device workspace for the cost kernels below (split-K Gram partials etc.). */
+int64_t trex_tree_workspace_bytes(int N, int64_t K);
+
+/* compute_surrogate_cost (tree.py:163-209): loss[0] and, when non-NULL,
+ * dS [N][K] = (diag(r+c) - (A+A^T)) S, dA [N][N] = (E_i+E_j)/2 - G_ij,
+ * G_out [N][N] = S S^T.  Gram and dS run on f32 MFMA. */
+int trex_tree_surrogate(const float* S, const float* A, int N, int64_t K, float* loss,
+                        float* dS, float* dA, float* G_out, void* workspace,
+                        int64_t workspace_bytes, void* stream);
+
+/* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
+ * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */
+int trex_tree_soft_cost(const float* S, const float* A, const float* C, int ckind, int N, int L,
+                        int Q, float* loss, float* W_scratch, void* workspace,
+                        int64_t workspace_bytes, void* stream);
+
+/* enforce_graph_constraints (tree.py:133-160): loss = [loss +]
+ * grad_scale * scale * sum_cols (colsum - 2)^2; dA (optional) +=
+ * grad_scale * 2 scale (colsum - 2) on the constrained block. */
+int trex_tree_constraint(const float* A, int N, float scale, float grad_scale, float* loss,
+                         int accumulate, float* dA, void* workspace, void* stream);
+
+/* compute_cost (tree.py:269-296): exact cost of a labelled tree. */
+int trex_tree_compute_cost(const float* S, const float* A, const float* subst, int N, int L,
+                           int Q, float* cost, void* workspace, void* stream);
+
+/* optax adam (b1, b2, eps, eps_root = 0) fused update of one tensor, step
+ * `count` (1-based); optional clip_by_global_norm(clip_norm) using squared
+ * norm partials from trex_sq_norm_parts over ALL gradient tensors. */
+int trex_adam_step(float* params, const float* grads, float* mu, float* nu, int64_t n,
+                   int count, float lr, float b1, float b2, float eps,
+                   const double* grad_sq_norm_parts, int n_parts, float clip_norm,
+                   void* stream);
+int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,189 @@
+"""GPU parity of the tree-cost path (trex tree.py) vs the fp64 oracle.
+
+Tolerances: f32 kernels vs fp64 oracle, rtol 1e-5 on losses / gradients
+(sums of up to ~1e6 f32 products, accumulated in fixed order), 1e-6 on
+elementwise softmaxes; exact for integer-valued results (compute_cost,
+one-hot surrogate = edge Hamming count).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import tree_ref as T
+from trex_amd import tree as G
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _t(x, device):
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float32, device=device)
+
+
+def _n(x):
+    return x.detach().cpu().numpy().astype(np.float64)
+
+
+def _tree_case(nl, L, Q, seed):
+    rng = np.random.default_rng(seed)
+    n = 2 * nl - 1
+    n_anc = nl - 1
+    params = {"tree_params": rng.normal(size=(n - 1, n_anc)).astype(np.float32),
+              "ancestors": rng.normal(size=(n_anc, L, Q)).astype(np.float32)}
+    noise = rng.gumbel(size=(n - 1, n_anc)).astype(np.float32)
+    seqs = np.zeros((n, L, Q), np.float32)
+    seqs[:nl] = np.eye(Q, dtype=np.float32)[rng.integers(0, Q, size=(nl, L))]
+    return params, noise, seqs
+
+
+def test_reference_tree_fixtures(device):
+    """tests/test_tree.py:18-87 fixtures, exact values."""
+    soft = np.array([[0.1, 0.9, 0.0], [0.8, 0.1, 0.1], [0.3, 0.3, 0.4]], np.float32)
+    oh = G.discretize_tree_topology(_t(soft, device), 3)
+    np.testing.assert_array_equal(_n(oh), T.discretize_tree_topology(soft, 3))
+    A = G.update_tree(_t(np.zeros((2, 1)), device), {"tree_params": _t(np.ones((2, 1)), device)})
+    np.testing.assert_allclose(_n(A), T.update_tree(np.ones((2, 1))), rtol=1e-6)
+    eye = G.update_tree(None, {"tree_params": torch.ones((1, 0), device=device)})
+    np.testing.assert_array_equal(_n(eye), np.eye(2))
+    assert float(G.enforce_graph_constraints(_t(np.eye(5), device), 10.0)) == 50.0
+    seqs = np.eye(4, dtype=np.float32)[np.array([[0, 1, 2], [3, 2, 1]])]
+    assert float(G.compute_surrogate_cost(_t(seqs, device), _t(np.eye(2), device))) == 0.0
+    s3 = np.eye(2, dtype=np.float32)[np.array([[0, 1], [1, 0], [0, 0]])]
+    c = float(G.compute_cost(_t(s3, device), _t(np.eye(3), device), _t(1 - np.eye(2), device)))
+    assert c == 0.0
+
+
+@pytest.mark.parametrize("T_", [1.0, 0.3, 2.0])
+def test_update_seq_and_vjp(device, T_):
+    params, _, seqs = _tree_case(8, 37, 4, 1)
+    S = G.update_seq({"ancestors": _t(params["ancestors"], device)}, _t(seqs, device), T_)
+    np.testing.assert_allclose(_n(S), T.update_seq(params["ancestors"], seqs, T_), rtol=1e-6,
+                               atol=1e-7)
+
+
+@pytest.mark.parametrize("nl,T_", [(4, 1.0), (16, 0.5), (100, 1.7)])
+def test_update_tree(device, nl, T_):
+    params, noise, _ = _tree_case(nl, 2, 4, nl)
+    gates = (np.random.default_rng(3).random(noise.shape) > 0.2).astype(np.float32)
+    for gt in (None, gates):
+        A = G.update_tree(_t(noise, device), {"tree_params": _t(params["tree_params"], device)},
+                          T_, None if gt is None else _t(gt, device))
+        ref = T.update_tree(params["tree_params"], noise, T_, gt)
+        np.testing.assert_allclose(_n(A), ref, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("N,L,Q", [(7, 3, 4), (15, 50, 4), (100, 33, 3), (129, 200, 4),
+                                   (64, 1000, 20)])
+def test_surrogate_value_and_grads(device, N, L, Q):
+    rng = np.random.default_rng(N + L)
+    S = rng.random((N, L, Q)).astype(np.float32)
+    A = rng.random((N, N)).astype(np.float32)
+    val, dS, dA = G.surrogate_cost_and_grads(_t(S, device), _t(A, device))
+    rv, rdS, rdA = T.compute_surrogate_cost_grads(S, A)
+    np.testing.assert_allclose(float(val), rv, rtol=RTOL)
+    np.testing.assert_allclose(_n(dS), rdS, rtol=RTOL, atol=RTOL * np.abs(rdS).max())
+    np.testing.assert_allclose(_n(dA), rdA, rtol=RTOL, atol=RTOL * np.abs(rdA).max())
+    np.testing.assert_allclose(float(G.compute_surrogate_cost(_t(S, device), _t(A, device))), rv,
+                               rtol=RTOL)
+
+
+def test_surrogate_onehot_is_edge_hamming_exact(device):
+    rng = np.random.default_rng(5)
+    nl, L, Q = 64, 2000, 4
+    n = 2 * nl - 1
+    seq = rng.integers(0, Q, size=(n, L))
+    S = np.eye(Q, dtype=np.float32)[seq]
+    parent = np.concatenate([nl + np.arange(nl) // 2, nl + (np.arange(nl - 2) + nl) // 2, [n - 1]])
+    A = np.eye(n, dtype=np.float32)[parent]
+    A[-1] = 0
+    ham = sum((seq[i] != seq[parent[i]]).sum() for i in range(n - 1))
+    assert float(G.compute_surrogate_cost(_t(S, device), _t(A, device))) == ham
+    A2 = np.eye(n, dtype=np.float32)[parent]
+    C = (1 - np.eye(Q)).astype(np.float32)
+    assert float(G.compute_cost(_t(S, device), _t(A2, device), _t(C, device))) == ham
+
+
+@pytest.mark.parametrize("ckind", ["none", "diag", "matrix"])
+def test_soft_cost(device, ckind):
+    rng = np.random.default_rng(7)
+    N, L, Q = 37, 41, 4
+    S = rng.random((N, L, Q)).astype(np.float32)
+    A = rng.random((N, N)).astype(np.float32)
+    C = {"none": None, "diag": rng.random(Q).astype(np.float32),
+         "matrix": rng.random((Q, Q)).astype(np.float32)}[ckind]
+    got = G.compute_soft_cost(_t(S, device), _t(A, device), None if C is None else _t(C, device))
+    np.testing.assert_allclose(float(got), T.compute_soft_cost(S, A, C), rtol=RTOL)
+
+
+def test_compute_cost_random_labels(device):
+    rng = np.random.default_rng(8)
+    N, L, Q = 31, 500, 4
+    S = rng.random((N, L, Q)).astype(np.float32)
+    A = rng.random((N, N)).astype(np.float32)
+    C = rng.integers(0, 5, size=(Q, Q)).astype(np.float32)
+    assert float(G.compute_cost(_t(S, device), _t(A, device), _t(C, device))) == \
+        T.compute_cost(S, A, C)
+
+
+@pytest.mark.parametrize("fix", ["none", "seqs", "tree"])
+def test_loss_and_grad_vs_oracle(device, fix):
+    params, noise, seqs = _tree_case(16, 60, 4, 11)
+    adj = T.discretize_tree_topology(T.update_tree(params["tree_params"], noise), 31)
+    Tt = 0.8
+    if fix == "seqs":
+        seqs = T.update_seq(params["ancestors"], seqs, Tt).astype(np.float32)
+    kw = dict(fix_seqs=fix == "seqs", fix_tree=fix == "tree")
+    loss, grads = G.loss_and_grad(_t(noise, device),
+                                  {k: _t(v, device) for k, v in params.items()},
+                                  _t(seqs, device), Tt, _t(adj, device), **kw)
+    rloss, rgrads = T.compute_loss(noise, params, seqs, Tt, adj, **kw)
+    np.testing.assert_allclose(float(loss), rloss, rtol=RTOL)
+    for k in ("tree_params", "ancestors"):
+        r = rgrads[k]
+        np.testing.assert_allclose(_n(grads[k]), r, rtol=RTOL, atol=RTOL * max(1.0, np.abs(r).max()))
+
+
+@pytest.mark.parametrize("clip", [None, 1.0])
+def test_adam_matches_optax_semantics(device, clip):
+    params, noise, seqs = _tree_case(8, 20, 4, 13)
+    p_dev = {k: _t(v, device) for k, v in params.items()}
+    p_ref = {k: v.astype(np.float64) for k, v in params.items()}
+    opt = G.Adam(p_dev, lr=0.01, clip_norm=clip)
+    st = T.adam_init(p_ref)
+    for step in range(5):
+        Tt = max(0.1, 2.0 * (1.0 - step / 5000))
+        _, g = G.loss_and_grad(_t(noise, device), p_dev, _t(seqs, device), Tt, None)
+        _, gr = T.compute_loss(noise, p_ref, seqs, Tt, None)
+        opt.step(p_dev, g)
+        upd, st = T.adam_update(gr, st, lr=0.01, clip_norm=clip)
+        p_ref = {k: p_ref[k] + upd[k] for k in p_ref}
+        for k in p_ref:
+            np.testing.assert_allclose(_n(p_dev[k]), p_ref[k], rtol=2e-5, atol=2e-6)
+
+
+def test_c5_scale_gram_properties(device):
+    """C5 shape (256 taxa -> 511 nodes, 50 000 sites, 4 states): the Gram-based
+    surrogate on one-hot sequences over a tree equals the edge Hamming count
+    (every Gram entry is an exact integer; the 19 M total is returned as the
+    correctly rounded f32), deterministic across runs."""
+    rng = np.random.default_rng(21)
+    nl, L, Q = 256, 50000, 4
+    n = 2 * nl - 1
+    seq = rng.integers(0, Q, size=(n, L)).astype(np.int64)
+    S = torch.nn.functional.one_hot(torch.as_tensor(seq, device=device), Q).to(torch.float32)
+    parent = np.concatenate([nl + np.arange(nl) // 2, nl + (np.arange(nl - 2) + nl) // 2, [n - 1]])
+    A = np.eye(n, dtype=np.float32)[parent]
+    A[-1] = 0
+    ham = int(sum((seq[i] != seq[parent[i]]).sum() for i in range(n - 1)))
+    v1, dS1, dA1 = G.surrogate_cost_and_grads(S, _t(A, device))
+    v2, dS2, dA2 = G.surrogate_cost_and_grads(S, _t(A, device))
+    assert float(v1) == float(np.float32(ham))
+    assert torch.equal(dS1, dS2) and torch.equal(dA1, dA2)
+    # dA_ij = (E_i + E_j)/2 - G_ij with one-hot rows: E = L, G_ij = #agreements
+    i, j = 3, parent[3]
+    agree = int((seq[i] == seq[j]).sum())
+    assert float(dA1[i, j]) == L - agree

@@ -44,6 +44,20 @@ SIGNATURES = {
                                     _p, _p, _p, _p, _p, _p, _p, _p, _c_i64, _p]),
     "trex_sankoff_backtrack": (_c_i, [_p, _c_i, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
     "trex_dp_to_trex_layout": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
+    # tree-cost path
+    "trex_tree_discretize": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _p]),
+    "trex_tree_update_seq": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _p, _p]),
+    "trex_tree_update_seq_bwd": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_f, _p, _p]),
+    "trex_tree_update_tree": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_f, _p, _p]),
+    "trex_tree_update_tree_bwd": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_f, _p, _p]),
+    "trex_tree_workspace_bytes": (_c_i64, [_c_i, _c_i64]),
+    "trex_tree_surrogate": (_c_i, [_p, _p, _c_i, _c_i64, _p, _p, _p, _p, _p, _c_i64, _p]),
+    "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),
+    "trex_tree_constraint": (_c_i, [_p, _c_i, _c_f, _c_f, _p, _c_i, _p, _p, _p]),
+    "trex_tree_compute_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _p, _p, _p]),
+    "trex_adam_step": (_c_i, [_p, _p, _p, _p, _c_i64, _c_i, _c_f, _c_f, _c_f, _c_f, _p, _c_i,
+                              _c_f, _p]),
+    "trex_sq_norm_parts": (_c_i, [_p, _c_i64, _p, _c_i, _p]),
 }
 
 

@@ -1,0 +1,801 @@
+// libtrexhip.so -- tree-cost kernels (maraxen/trex src/trex/tree.py) for gfx950.
+//
+//  a12 update_seq      (tree.py:110-130)  state softmax, fwd + VJP
+//  a11 update_tree     (tree.py:50-107)   masked row softmax, fwd + VJP
+//  a9  compute_surrogate_cost (tree.py:163-209): G = F F^T (MFMA f32, split-K),
+//      loss / dA / M = diag(r+c) - (A+A^T) (one combine pass), dF = M F (MFMA)
+//  a10 compute_soft_cost (tree.py:212-266): W = S C per site, G = F W^T
+//  a13 enforce_graph_constraints (tree.py:133-160), fwd + grad
+//  a8  compute_cost    (tree.py:269-296)  gather-reduce
+//  a14 optax adam (+ clip_by_global_norm) fused update
+//
+// GEMMs run on v_mfma_f32_32x32x2_f32 (exact f32 fmaf chains; gfx950 has no
+// reduced-precision f32 path).  All reductions are fixed-order (fp64), so
+// results are bitwise reproducible.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "trex_common.h"
+
+namespace trex {
+namespace {
+
+constexpr int kWave = 64;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+int tree_hip_check(const char* fn) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return TREX_OK;
+}
+
+__device__ __forceinline__ double block_sum_256(double v, double* sh) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// a12 update_seq: S = softmax_q(T * X) per (ancestor, site)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void update_seq_kernel(const float* __restrict__ x, int64_t rows,
+                                                        int Q, float T, float* __restrict__ s) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const float* xr = x + r * Q;
+    float* sr = s + r * Q;
+    float m = -INFINITY;
+    for (int q = 0; q < Q; ++q) m = fmaxf(m, xr[q] * T);
+    float sum = 0.0f;
+    for (int q = 0; q < Q; ++q) {
+      const float e = expf(xr[q] * T - m);
+      sr[q] = e;
+      sum += e;
+    }
+    const float inv = 1.0f / sum;
+    for (int q = 0; q < Q; ++q) sr[q] *= inv;
+  }
+}
+
+__global__ __launch_bounds__(256) void update_seq_bwd_kernel(const float* __restrict__ s,
+                                                            const float* __restrict__ ds,
+                                                            int64_t rows, int Q, float T,
+                                                            float* __restrict__ dx) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const float* sr = s + r * Q;
+    const float* gr = ds + r * Q;
+    float dot = 0.0f;
+    for (int q = 0; q < Q; ++q) dot = fmaf(sr[q], gr[q], dot);
+    for (int q = 0; q < Q; ++q) dx[r * Q + q] = T * sr[q] * (gr[q] - dot);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// a11 update_tree: logits z (masked), A = row softmax.  One block per row.
+//   theta/noise/gates [N-1][n_anc]; A [N][N]
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float tree_logit(const float* theta, const float* noise,
+                                            const float* gates, int N, int n_anc, float T, int i,
+                                            int j, bool* valid) {
+  const int nl = N - n_anc;
+  *valid = false;
+  if (i == N - 1) {
+    if (j == N - 1) { *valid = true; return 1.0f; }
+    return -INFINITY;
+  }
+  if (j < nl) return -INFINITY;
+  const int ja = j - nl;
+  if (i >= nl && !(ja > i - nl)) return -INFINITY;  // ancestor block: upper triangular
+  const size_t k = (size_t)i * n_anc + ja;
+  float p = theta[k] + (noise ? noise[k] : 0.0f);
+  if (gates) p *= gates[k];
+  *valid = true;
+  return p / T;
+}
+
+__global__ __launch_bounds__(256) void update_tree_kernel(const float* __restrict__ theta,
+                                                         const float* __restrict__ noise,
+                                                         const float* __restrict__ gates, int N,
+                                                         int n_anc, float T, float* __restrict__ A) {
+  __shared__ float red[256];
+  const int i = blockIdx.x;
+  float m = -INFINITY;
+  for (int j = threadIdx.x; j < N; j += 256) {
+    bool v;
+    m = fmaxf(m, tree_logit(theta, noise, gates, N, n_anc, T, i, j, &v));
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  m = red[0];
+  __syncthreads();
+  float s = 0.0f;
+  for (int j = threadIdx.x; j < N; j += 256) {
+    bool v;
+    const float z = tree_logit(theta, noise, gates, N, n_anc, T, i, j, &v);
+    const float e = v ? expf(z - m) : 0.0f;
+    A[(size_t)i * N + j] = e;
+    s += e;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float inv = 1.0f / red[0];
+  for (int j = threadIdx.x; j < N; j += 256) A[(size_t)i * N + j] *= inv;
+}
+
+__global__ __launch_bounds__(256) void update_tree_bwd_kernel(const float* __restrict__ A,
+                                                             const float* __restrict__ dA,
+                                                             const float* __restrict__ gates,
+                                                             int N, int n_anc, float T,
+                                                             float* __restrict__ dtheta) {
+  __shared__ double sh[256];
+  const int i = blockIdx.x;  // rows 0..N-2
+  const int nl = N - n_anc;
+  double dot = 0.0;
+  for (int j = threadIdx.x; j < N; j += 256)
+    dot += (double)A[(size_t)i * N + j] * (double)dA[(size_t)i * N + j];
+  const float d = (float)block_sum_256(dot, sh);
+  for (int ja = threadIdx.x; ja < n_anc; ja += 256) {
+    const int j = nl + ja;
+    const bool valid = (i < nl) || (ja > i - nl);
+    float g = 0.0f;
+    if (valid) {
+      const float a = A[(size_t)i * N + j];
+      g = a * (dA[(size_t)i * N + j] - d) / T;
+      if (gates) g *= gates[(size_t)i * n_anc + ja];
+    }
+    dtheta[(size_t)i * n_anc + ja] = g;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// a9 Gram G = X Y^T on MFMA f32 (X, Y: [N][K] row-major).  One wave computes
+// a 64x64 tile (2x2 32x32 accumulators) over one K slice.  Lane l (row
+// r = l&31, half h = l>>5) loads 16 consecutive k of its row per fragment;
+// MFMA t then covers k = kb + t and kb + 16 + t on the two halves (the k
+// permutation is the same for X and Y, so the dot products are exact).
+// Blocks are grouped so that one XCD (blockIdx % 8) walks the tiles of one
+// K slice while that slice is L2-resident.
+// ---------------------------------------------------------------------------
+// 16 consecutive k of one row (row stride K), zero past kend / nrows
+__device__ __forceinline__ void load_frag16(const float* __restrict__ base, int row, int nrows,
+                                            int K, int k0, int kend, float (&o)[16]) {
+  if (row < nrows && k0 + 16 <= kend && (K & 3) == 0) {
+    const float4* p = reinterpret_cast<const float4*>(base + (size_t)row * K + k0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float4 v = p[t];
+      o[4 * t] = v.x; o[4 * t + 1] = v.y; o[4 * t + 2] = v.z; o[4 * t + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      o[t] = (row < nrows && k0 + t < kend) ? base[(size_t)row * K + k0 + t] : 0.0f;
+  }
+}
+
+__device__ __forceinline__ void pair_tiles(int pair, int ntile, int symmetric, int* ti, int* tj) {
+  if (symmetric) {  // (ti <= tj), row-major over the upper triangle
+    int a = 0, rem = pair;
+    while (rem >= ntile - a) { rem -= ntile - a; ++a; }
+    *ti = a;
+    *tj = a + rem;
+  } else {
+    *ti = pair / ntile;
+    *tj = pair % ntile;
+  }
+}
+
+__global__ __launch_bounds__(kWave) void gram_kernel(const float* __restrict__ X,
+                                                    const float* __restrict__ Y, int N, int K,
+                                                    int ntile, int npairs, int symmetric,
+                                                    int ksplit, int kslice,
+                                                    float* __restrict__ part) {
+  const int b = blockIdx.x;
+  const int xcd = b & 7, m = b >> 3;
+  const int split = (m / npairs) * 8 + xcd;
+  const int pair = m % npairs;
+  if (split >= ksplit) return;
+  int ti, tj;
+  pair_tiles(pair, ntile, symmetric, &ti, &tj);
+  const int lane = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const int k_lo = split * kslice, k_hi = min(K, k_lo + kslice);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[u][v] = (f32x16){};
+  for (int kb = k_lo; kb < k_hi; kb += 32) {
+    float xa[2][16], yb[2][16];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) load_frag16(X, ti * 64 + u * 32 + r, N, K, kb + 16 * h, k_hi, xa[u]);
+#pragma unroll
+    for (int v = 0; v < 2; ++v) load_frag16(Y, tj * 64 + v * 32 + r, N, K, kb + 16 * h, k_hi, yb[v]);
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[u][t], yb[v][t], acc[u][v], 0, 0, 0);
+  }
+  // partial tile [split][pair][64][64]
+  float* out = part + ((size_t)split * npairs + pair) * 64 * 64;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+        out[(u * 32 + row) * 64 + v * 32 + r] = acc[u][v][q];
+      }
+}
+
+// G[i][j] = sum over splits (fixed order, fp64); symmetric tiles mirrored
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ part, int N,
+                                                         int ntile, int npairs, int ksplit,
+                                                         int symmetric, float* __restrict__ G) {
+  const size_t total = (size_t)npairs * 4096;
+  for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const int pair = (int)(t / 4096);
+    const int e = (int)(t % 4096);
+    int ti, tj;
+    pair_tiles(pair, ntile, symmetric, &ti, &tj);
+    double s = 0.0;
+    for (int sp = 0; sp < ksplit; ++sp) s += (double)part[((size_t)sp * npairs + pair) * 4096 + e];
+    const int i = ti * 64 + e / 64, j = tj * 64 + e % 64;
+    if (i < N && j < N) {
+      G[(size_t)i * N + j] = (float)s;
+      if (symmetric) G[(size_t)j * N + i] = (float)s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// a9 combine: per row i (one block): rowloss_i, dA row, M row.
+//   loss = sum_ij A_ij (G_ii + G_jj - 2 G_ij) / 2 ; dA_ij = (G_ii+G_jj)/2 - G_ij
+//   M = diag(r + c) - (A + A^T)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void surrogate_combine_kernel(const float* __restrict__ A,
+                                                               const float* __restrict__ G, int N,
+                                                               float* __restrict__ dA,
+                                                               float* __restrict__ M,
+                                                               double* __restrict__ rowloss) {
+  __shared__ double sh[256];
+  const int i = blockIdx.x;
+  const float gii = G[(size_t)i * N + i];
+  double l = 0.0, rs = 0.0, cs = 0.0;
+  for (int j = threadIdx.x; j < N; j += 256) {
+    const float a = A[(size_t)i * N + j];
+    const float at = A[(size_t)j * N + i];
+    const float gjj = G[(size_t)j * N + j];
+    const float gij = G[(size_t)i * N + j];
+    l += (double)a * ((double)gii + (double)gjj - 2.0 * (double)gij);
+    rs += a;
+    cs += at;
+    if (dA) dA[(size_t)i * N + j] = 0.5f * (gii + gjj) - gij;
+  }
+  const double L = block_sum_256(l, sh);
+  const double rc = block_sum_256(rs, sh) + block_sum_256(cs, sh);
+  if (threadIdx.x == 0) rowloss[i] = 0.5 * L;
+  if (M) {
+    for (int j = threadIdx.x; j < N; j += 256) {
+      const float a = A[(size_t)i * N + j] + A[(size_t)j * N + i];
+      M[(size_t)i * N + j] = (i == j ? (float)rc : 0.0f) - a;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict__ v, int n,
+                                                      float scale, float* __restrict__ out,
+                                                      int accumulate) {
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int t = threadIdx.x; t < n; t += 256) s += v[t];
+  s = block_sum_256(s, sh);
+  if (threadIdx.x == 0) out[0] = (accumulate ? out[0] : 0.0f) + (float)(s * scale);
+}
+
+// ---------------------------------------------------------------------------
+// a9 dF = M F  (M [N][N], F [N][K]) on MFMA f32.  One wave = 64 rows x 64
+// columns of dF; reduction over all N inside.  A operand: M rows via float4
+// (k permutation kb + 4h + t), B operand: F rows kb + 4h + t (coalesced).
+// Column blocks are XCD-grouped: the 8 row tiles of a column block share an
+// XCD, so each F block leaves HBM once.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWave) void mf_kernel(const float* __restrict__ Mm,
+                                                  const float* __restrict__ F, int N, int K,
+                                                  int nrowt, int ncolb, float* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int xcd = b & 7, m = b >> 3;
+  const int rt = m % nrowt;
+  const int cb = (m / nrowt) * 8 + xcd;
+  if (cb >= ncolb) return;
+  const int lane = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const int c0 = cb * 64;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[u][v] = (f32x16){};
+  for (int nb = 0; nb < N; nb += 8) {
+    float ma[2][4], fb[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = rt * 64 + u * 32 + r;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = nb + 4 * h + t;
+        ma[u][t] = (row < N && n < N) ? Mm[(size_t)row * N + n] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int col = c0 + v * 32 + r;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int n = nb + 4 * h + t;
+        fb[v][t] = (n < N && col < K) ? F[(size_t)n * K + col] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(ma[u][t], fb[v][t], acc[u][v], 0, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = rt * 64 + u * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const int col = c0 + v * 32 + r;
+        if (row < N && col < K) out[(size_t)row * K + col] = acc[u][v][q];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// a10 W = S C per (node, site):  ckind 0: W = S; 1: W = S * c (vector);
+//     2: W = S @ C (matrix, w_j = sum_q s_q C[q][j])
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void weight_seq_kernel(const float* __restrict__ S, int64_t rows,
+                                                        int Q, const float* __restrict__ C,
+                                                        int ckind, float* __restrict__ W) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const float* s = S + r * Q;
+    for (int j = 0; j < Q; ++j) {
+      float w;
+      if (ckind == 0) {
+        w = s[j];
+      } else if (ckind == 1) {
+        w = s[j] * C[j];
+      } else {
+        w = 0.0f;
+        for (int q = 0; q < Q; ++q) w = fmaf(s[q], C[q * Q + j], w);
+      }
+      W[r * Q + j] = w;
+    }
+  }
+}
+
+// soft-cost combine: loss_i = sum_j A_ij (E_i + E_j - 2 G_ij) / 2, E = diag(G)
+// (E_i = sum S_i * W_i = <S_i, W_i>, tree.py:255)
+__global__ __launch_bounds__(256) void soft_combine_kernel(const float* __restrict__ A,
+                                                          const float* __restrict__ G, int N,
+                                                          double* __restrict__ rowloss) {
+  __shared__ double sh[256];
+  const int i = blockIdx.x;
+  const double ei = G[(size_t)i * N + i];
+  double l = 0.0;
+  for (int j = threadIdx.x; j < N; j += 256)
+    l += (double)A[(size_t)i * N + j] *
+         (ei + (double)G[(size_t)j * N + j] - 2.0 * (double)G[(size_t)i * N + j]);
+  l = block_sum_256(l, sh);
+  if (threadIdx.x == 0) rowloss[i] = 0.5 * l;
+}
+
+// ---------------------------------------------------------------------------
+// a13 constraint: scale * sum_cols (sum_{i<N-1} A[i][c] - 2)^2, c in last n_anc
+//   grad (x gscale, accumulated into dA): 2 scale (colsum - 2)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void constraint_kernel(const float* __restrict__ A, int N,
+                                                        float scale, float gscale,
+                                                        double* __restrict__ colloss,
+                                                        float* __restrict__ dA) {
+  __shared__ double sh[256];
+  const int n_anc = (N - 1) / 2;
+  const int c = N - n_anc + blockIdx.x;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < N - 1; i += 256) s += A[(size_t)i * N + c];
+  s = block_sum_256(s, sh);
+  const double dev = s - 2.0;
+  if (threadIdx.x == 0) colloss[blockIdx.x] = (double)scale * dev * dev;
+  if (dA) {
+    const float g = (float)(2.0 * scale * dev) * gscale;
+    for (int i = threadIdx.x; i < N - 1; i += 256) dA[(size_t)i * N + c] += g;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// a8 compute_cost: seq = argmax_q S, parent = argmax_j A (first index), sum
+//   subst[seq[parent][l]][seq[i][l]] over i < N-1, l.  One block per node i.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void compute_cost_kernel(const float* __restrict__ S,
+                                                          const float* __restrict__ A,
+                                                          const float* __restrict__ subst, int N,
+                                                          int L, int Q,
+                                                          double* __restrict__ rowcost) {
+  __shared__ double sh[256];
+  __shared__ float bv[256];
+  __shared__ int bi[256];
+  const int i = blockIdx.x;
+  // parent = first argmax of row i
+  float best = -INFINITY;
+  int arg = 0x7FFFFFFF;
+  for (int j = threadIdx.x; j < N; j += 256) {
+    const float v = A[(size_t)i * N + j];
+    if (v > best || (v == best && j < arg)) { best = v; arg = j; }
+  }
+  bv[threadIdx.x] = best;
+  bi[threadIdx.x] = arg;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const float v = bv[threadIdx.x + w];
+      const int k = bi[threadIdx.x + w];
+      if (v > bv[threadIdx.x] || (v == bv[threadIdx.x] && k < bi[threadIdx.x])) {
+        bv[threadIdx.x] = v;
+        bi[threadIdx.x] = k;
+      }
+    }
+    __syncthreads();
+  }
+  const int p = bi[0] == 0x7FFFFFFF ? 0 : bi[0];
+  double s = 0.0;
+  for (int l = threadIdx.x; l < L; l += 256) {
+    const float* si = S + ((size_t)i * L + l) * Q;
+    const float* sp = S + ((size_t)p * L + l) * Q;
+    int a = 0, c = 0;
+    float va = si[0], vc = sp[0];
+    for (int q = 1; q < Q; ++q) {
+      if (si[q] > va) { va = si[q]; a = q; }
+      if (sp[q] > vc) { vc = sp[q]; c = q; }
+    }
+    s += subst[c * Q + a];
+  }
+  s = block_sum_256(s, sh);
+  if (threadIdx.x == 0) rowcost[i] = s;
+}
+
+// ---------------------------------------------------------------------------
+// a14 optax adam (b1, b2, eps; eps_root = 0) with optional global-norm clip
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sq_norm_kernel(const float* __restrict__ g, int64_t n,
+                                                     double* __restrict__ part) {
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256)
+    s += (double)g[t] * (double)g[t];
+  s = block_sum_256(s, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
+                                                  const float* __restrict__ g,
+                                                  float* __restrict__ mu, float* __restrict__ nu,
+                                                  int64_t n, float lr, float b1, float b2,
+                                                  float eps, float bc1, float bc2,
+                                                  const double* __restrict__ sqnorm,
+                                                  int nparts, float clip) {
+  float scale = 1.0f;
+  if (sqnorm) {
+    double s = 0.0;
+    for (int k = 0; k < nparts; ++k) s += sqnorm[k];  // same fixed order in every thread
+    const float norm = (float)sqrt(s);
+    if (!(norm < clip)) scale = clip / norm;
+  }
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const float gt = (scale == 1.0f) ? g[t] : (g[t] / (clip / scale)) * clip;
+    const float m = (1.0f - b1) * gt + b1 * mu[t];
+    const float v = (1.0f - b2) * (gt * gt) + b2 * nu[t];
+    mu[t] = m;
+    nu[t] = v;
+    const float mh = m / bc1;
+    const float vh = v / bc2;
+    p[t] = p[t] + (-lr) * (mh / (sqrtf(vh) + eps));
+  }
+}
+
+__global__ __launch_bounds__(256) void identity_kernel(int N, float* __restrict__ A) {
+  const size_t total = (size_t)N * N;
+  for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256)
+    A[t] = (t / N == t % N) ? 1.0f : 0.0f;
+}
+
+// discretize_tree_topology: one_hot(argmax(A[i]), n_nodes), first index on ties
+__global__ __launch_bounds__(256) void discretize_kernel(const float* __restrict__ A, int ncols,
+                                                        int n_nodes, float* __restrict__ out) {
+  __shared__ float bv[256];
+  __shared__ int bi[256];
+  const int i = blockIdx.x;
+  float best = -INFINITY;
+  int arg = 0x7FFFFFFF;
+  for (int j = threadIdx.x; j < ncols; j += 256) {
+    const float v = A[(size_t)i * ncols + j];
+    if (v > best || (v == best && j < arg)) { best = v; arg = j; }
+  }
+  bv[threadIdx.x] = best;
+  bi[threadIdx.x] = arg;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      const float v = bv[threadIdx.x + w];
+      const int k = bi[threadIdx.x + w];
+      if (v > bv[threadIdx.x] || (v == bv[threadIdx.x] && k < bi[threadIdx.x])) {
+        bv[threadIdx.x] = v;
+        bi[threadIdx.x] = k;
+      }
+    }
+    __syncthreads();
+  }
+  const int a = bi[0] == 0x7FFFFFFF ? 0 : bi[0];
+  for (int j = threadIdx.x; j < n_nodes; j += 256) out[(size_t)i * n_nodes + j] = (j == a) ? 1.0f : 0.0f;
+}
+
+int grid_for(int64_t n, int per = 256, int cap = 8192) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, cap));
+}
+
+}  // namespace
+}  // namespace trex
+
+using namespace trex;
+
+extern "C" int trex_tree_update_seq(const float* x, int n_anc, int L, int Q, float T, float* s,
+                                    void* stream) {
+  if (!x || !s || n_anc < 0 || L <= 0 || Q <= 0)
+    return set_error(TREX_E_ARG, "trex_tree_update_seq: bad arguments");
+  const int64_t rows = (int64_t)n_anc * L;
+  if (rows == 0) return TREX_OK;
+  hipLaunchKernelGGL(update_seq_kernel, dim3(grid_for(rows)), dim3(256), 0, (hipStream_t)stream,
+                     x, rows, Q, T, s);
+  return tree_hip_check("trex_tree_update_seq");
+}
+
+extern "C" int trex_tree_update_seq_bwd(const float* s, const float* ds, int n_anc, int L, int Q,
+                                        float T, float* dx, void* stream) {
+  if (!s || !ds || !dx || n_anc < 0 || L <= 0 || Q <= 0)
+    return set_error(TREX_E_ARG, "trex_tree_update_seq_bwd: bad arguments");
+  const int64_t rows = (int64_t)n_anc * L;
+  if (rows == 0) return TREX_OK;
+  hipLaunchKernelGGL(update_seq_bwd_kernel, dim3(grid_for(rows)), dim3(256), 0,
+                     (hipStream_t)stream, s, ds, rows, Q, T, dx);
+  return tree_hip_check("trex_tree_update_seq_bwd");
+}
+
+extern "C" int trex_tree_update_tree(const float* theta, const float* noise, const float* gates,
+                                     int N, int n_anc, float T, float* A, void* stream) {
+  if (!A || N < 2 || n_anc < 0 || n_anc >= N || !(T > 0.0f))
+    return set_error(TREX_E_ARG, "trex_tree_update_tree: bad arguments");
+  if (n_anc > 0 && !theta) return set_error(TREX_E_ARG, "trex_tree_update_tree: theta is NULL");
+  if (n_anc == 0) {  // tree.py:68-69: identity
+    hipLaunchKernelGGL(identity_kernel, dim3(grid_for((int64_t)N * N)), dim3(256), 0,
+                       (hipStream_t)stream, N, A);
+    return tree_hip_check("trex_tree_update_tree");
+  }
+  hipLaunchKernelGGL(update_tree_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, theta, noise,
+                     gates, N, n_anc, T, A);
+  return tree_hip_check("trex_tree_update_tree");
+}
+
+extern "C" int trex_tree_update_tree_bwd(const float* A, const float* dA, const float* gates,
+                                         int N, int n_anc, float T, float* dtheta, void* stream) {
+  if (!A || !dA || !dtheta || N < 2 || n_anc <= 0 || n_anc >= N || !(T > 0.0f))
+    return set_error(TREX_E_ARG, "trex_tree_update_tree_bwd: bad arguments");
+  hipLaunchKernelGGL(update_tree_bwd_kernel, dim3(N - 1), dim3(256), 0, (hipStream_t)stream, A,
+                     dA, gates, N, n_anc, T, dtheta);
+  return tree_hip_check("trex_tree_update_tree_bwd");
+}
+
+namespace {
+struct GramPlan {
+  int ntile, npairs, ksplit, kslice;
+};
+GramPlan gram_plan(int N, int64_t K, bool symmetric = false) {
+  GramPlan g;
+  g.ntile = (N + 63) / 64;
+  // workspace is sized for the full (non-symmetric) tile set
+  g.npairs = symmetric ? g.ntile * (g.ntile + 1) / 2 : g.ntile * g.ntile;
+  // enough waves to fill 256 CUs several times; slices multiple of 32
+  int ks = (int)std::max<int64_t>(1, std::min<int64_t>(256, (4096 + g.npairs - 1) / g.npairs));
+  ks = (ks + 7) / 8 * 8;
+  int64_t slice = (K + ks - 1) / ks;
+  slice = (slice + 31) / 32 * 32;
+  g.kslice = (int)std::max<int64_t>(32, slice);
+  g.ksplit = (int)((K + g.kslice - 1) / g.kslice);
+  return g;
+}
+}  // namespace
+
+namespace {
+// split-K partial buffer: the larger of the symmetric and full tile plans
+int64_t part_bytes(int N, int64_t K) {
+  int64_t b = 0;
+  for (bool sym : {true, false}) {
+    const GramPlan g = gram_plan(N, K, sym);
+    b = std::max<int64_t>(b, (int64_t)((g.ksplit + 7) / 8 * 8) * g.npairs * 4096 * 4);
+  }
+  return b;
+}
+}  // namespace
+
+extern "C" int64_t trex_tree_workspace_bytes(int N, int64_t K) {
+  if (N <= 0 || K <= 0) return 0;
+  const int64_t part = part_bytes(N, K);
+  const int64_t mats = (int64_t)N * N * 4 * 2;   // G, M
+  const int64_t rows = (int64_t)N * 8 * 2 + 8192 * 8;  // row losses / E / norm parts
+  return part + mats + rows + 1024;
+}
+
+namespace {
+int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
+         hipStream_t st) {
+  const GramPlan g = gram_plan(N, K, symmetric != 0);
+  const int ks8 = (g.ksplit + 7) / 8 * 8;
+  const int blocks = g.npairs * ks8;
+  hipLaunchKernelGGL(gram_kernel, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
+                     g.npairs, symmetric, g.ksplit, g.kslice, part);
+  const size_t total = (size_t)g.npairs * 4096;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(grid_for((int64_t)total)), dim3(256), 0, st, part, N,
+                     g.ntile, g.npairs, g.ksplit, symmetric, G);
+  return tree_hip_check("gram");
+}
+}  // namespace
+
+extern "C" int trex_tree_surrogate(const float* S, const float* A, int N, int64_t K, float* loss,
+                                   float* dS, float* dA, float* G_out, void* workspace,
+                                   int64_t workspace_bytes, void* stream) {
+  if (!S || !A || !loss || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF)
+    return set_error(TREX_E_ARG, "trex_tree_surrogate: bad arguments");
+  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
+    return set_error(TREX_E_ARG, "trex_tree_surrogate: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  char* w = static_cast<char*>(workspace);
+  float* part = reinterpret_cast<float*>(w);
+  w += part_bytes(N, K);
+  float* G = reinterpret_cast<float*>(w);
+  w += (int64_t)N * N * 4;
+  float* M = reinterpret_cast<float*>(w);
+  w += (int64_t)N * N * 4;
+  double* rowloss = reinterpret_cast<double*>(w);
+  if (int e = gram(S, S, N, K, 1, G, part, st)) return e;
+  hipLaunchKernelGGL(surrogate_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, dA,
+                     dS ? M : nullptr, rowloss);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0);
+  if (dS) {
+    const int nrowt = (N + 63) / 64;
+    const int ncolb = (int)((K + 63) / 64);
+    const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
+    hipLaunchKernelGGL(mf_kernel, dim3(blocks), dim3(kWave), 0, st, M, S, N, (int)K, nrowt, ncolb,
+                       dS);
+  }
+  if (G_out &&
+      hipMemcpyAsync(G_out, G, sizeof(float) * (size_t)N * N, hipMemcpyDeviceToDevice, st) !=
+          hipSuccess)
+    return tree_hip_check("trex_tree_surrogate(G)");
+  return tree_hip_check("trex_tree_surrogate");
+}
+
+extern "C" int trex_tree_soft_cost(const float* S, const float* A, const float* C, int ckind,
+                                   int N, int L, int Q, float* loss, float* W_scratch,
+                                   void* workspace, int64_t workspace_bytes, void* stream) {
+  const int64_t K = (int64_t)L * Q;
+  if (!S || !A || !loss || !workspace || N <= 0 || L <= 0 || Q <= 0 || ckind < 0 || ckind > 2 ||
+      (ckind > 0 && !C) || (ckind > 0 && !W_scratch))
+    return set_error(TREX_E_ARG, "trex_tree_soft_cost: bad arguments");
+  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
+    return set_error(TREX_E_ARG, "trex_tree_soft_cost: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  char* w = static_cast<char*>(workspace);
+  float* part = reinterpret_cast<float*>(w);
+  w += part_bytes(N, K);
+  float* G = reinterpret_cast<float*>(w);
+  w += (int64_t)N * N * 8;
+  double* rowloss = reinterpret_cast<double*>(w);
+  const float* Wp = S;
+  if (ckind > 0) {
+    const int64_t rows = (int64_t)N * L;
+    hipLaunchKernelGGL(weight_seq_kernel, dim3(grid_for(rows)), dim3(256), 0, st, S, rows, Q, C,
+                       ckind, W_scratch);
+    Wp = W_scratch;
+  }
+  // G[i][j] = <S_i, W_j> (not symmetric for a general C): all tile pairs
+  if (int e = gram(S, Wp, N, K, ckind == 0 ? 1 : 0, G, part, st)) return e;
+  hipLaunchKernelGGL(soft_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, rowloss);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0);
+  return tree_hip_check("trex_tree_soft_cost");
+}
+
+extern "C" int trex_tree_constraint(const float* A, int N, float scale, float grad_scale,
+                                    float* loss, int accumulate, float* dA, void* workspace,
+                                    void* stream) {
+  if (!A || !loss || !workspace || N < 3)
+    return set_error(TREX_E_ARG, "trex_tree_constraint: bad arguments");
+  const int n_anc = (N - 1) / 2;
+  hipStream_t st = (hipStream_t)stream;
+  double* colloss = static_cast<double*>(workspace);
+  hipLaunchKernelGGL(constraint_kernel, dim3(n_anc), dim3(256), 0, st, A, N, scale, grad_scale,
+                     colloss, dA);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, colloss, n_anc, grad_scale,
+                     loss, accumulate);
+  return tree_hip_check("trex_tree_constraint");
+}
+
+extern "C" int trex_tree_compute_cost(const float* S, const float* A, const float* subst, int N,
+                                      int L, int Q, float* cost, void* workspace, void* stream) {
+  if (!S || !A || !subst || !cost || !workspace || N < 2 || L <= 0 || Q <= 0)
+    return set_error(TREX_E_ARG, "trex_tree_compute_cost: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  double* rowcost = static_cast<double*>(workspace);
+  // rows 0..N-2 only ([:-1] in tree.py:296)
+  hipLaunchKernelGGL(compute_cost_kernel, dim3(N - 1), dim3(256), 0, st, S, A, subst, N, L, Q,
+                     rowcost);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowcost, N - 1, 1.0f, cost, 0);
+  return tree_hip_check("trex_tree_compute_cost");
+}
+
+extern "C" int trex_adam_step(float* params, const float* grads, float* mu, float* nu, int64_t n,
+                              int count, float lr, float b1, float b2, float eps,
+                              const double* grad_sq_norm_parts, int n_parts, float clip_norm,
+                              void* stream) {
+  if (!params || !grads || !mu || !nu || n < 0 || count < 1)
+    return set_error(TREX_E_ARG, "trex_adam_step: bad arguments");
+  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
+  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, params,
+                     grads, mu, nu, n, lr, b1, b2, eps, bc1, bc2, grad_sq_norm_parts, n_parts,
+                     clip_norm);
+  return tree_hip_check("trex_adam_step");
+}
+
+extern "C" int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts,
+                                  void* stream) {
+  if (!x || !parts || n_parts <= 0 || n_parts > 8192)
+    return set_error(TREX_E_ARG, "trex_sq_norm_parts: bad arguments");
+  hipLaunchKernelGGL(sq_norm_kernel, dim3(n_parts), dim3(256), 0, (hipStream_t)stream, x, n,
+                     parts);
+  return tree_hip_check("trex_sq_norm_parts");
+}
+
+extern "C" int trex_tree_discretize(const float* A, int nrows, int ncols, int n_nodes, float* out,
+                                    void* stream) {
+  if (!A || !out || nrows <= 0 || ncols <= 0 || n_nodes <= 0)
+    return set_error(TREX_E_ARG, "trex_tree_discretize: bad arguments");
+  hipLaunchKernelGGL(discretize_kernel, dim3(nrows), dim3(256), 0, (hipStream_t)stream, A, ncols,
+                     n_nodes, out);
+  return tree_hip_check("trex_tree_discretize");
+}

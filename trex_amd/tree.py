@@ -1,0 +1,277 @@
+"""trex's ``tree`` module on MI355X.
+
+Mirrors maraxen/trex ``src/trex/tree.py``:
+* ``discretize_tree_topology`` (:31-47), ``update_tree`` (:50-107),
+  ``update_seq`` (:110-130);
+* ``enforce_graph_constraints`` (:133-160), ``compute_surrogate_cost``
+  (:163-209), ``compute_soft_cost`` (:212-266), ``compute_cost`` (:269-296);
+* ``compute_loss`` (:299-361).
+
+It adds what the reference gets from jax.grad and optax: ``loss_and_grad``
+(analytic reverse mode on the same kernels) and ``Adam`` (optax.adam /
+clip_by_global_norm semantics, src/trex/evals/benchmark.py:41-72).
+
+One interface change: ``update_tree`` takes its Gumbel noise explicitly
+(``noise`` instead of a JAX PRNG key), since trex's threefry stream
+(tree.py:71) is JAX-specific.  ``gumbel_noise`` draws one with torch.
+All arithmetic runs in libtrexhip.so.
+"""
+
+from __future__ import annotations
+
+from ._lib import check, lib, ptr, stream_handle
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _dev(x, device=None):
+    torch = _torch()
+    t = torch.as_tensor(x)
+    if device is None:
+        device = t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+_WS: dict = {}
+
+
+def _workspace(N, K, device):
+    torch = _torch()
+    nbytes = int(lib().trex_tree_workspace_bytes(N, K))
+    key = str(device)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = ws
+    return ws
+
+
+def gumbel_noise(shape, generator=None, device=None):
+    """Standard Gumbel noise (what jax.random.gumbel draws at tree.py:71)."""
+    torch = _torch()
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    u = torch.rand(shape, generator=generator, device=device, dtype=torch.float32)
+    return -torch.log(-torch.log(u.clamp_min(1e-20)))
+
+
+# ---------------------------------------------------------------------------
+# topology / sequences
+# ---------------------------------------------------------------------------
+def discretize_tree_topology(adjacency, n_nodes: int):
+    """one_hot(argmax(adjacency, 1)) (tree.py:46-47), first index on ties."""
+    torch = _torch()
+    A = _dev(adjacency)
+    out = torch.empty((A.shape[0], n_nodes), dtype=torch.float32, device=A.device)
+    check(lib().trex_tree_discretize(ptr(A), A.shape[0], A.shape[1], n_nodes, ptr(out),
+                                     stream_handle(A.device)))
+    return out
+
+
+def update_tree(noise, params, temperature: float = 1.0, gates=None):
+    """Relaxed topology: row softmax of the masked logits (tree.py:50-107)."""
+    torch = _torch()
+    theta = _dev(params["tree_params"])
+    n_m1, n_anc = theta.shape
+    N = n_m1 + 1
+    dev = theta.device
+    nz = _dev(noise, dev) if noise is not None else None
+    gt = _dev(gates, dev) if gates is not None else None
+    A = torch.empty((N, N), dtype=torch.float32, device=dev)
+    check(lib().trex_tree_update_tree(ptr(theta), ptr(nz), ptr(gt), N, n_anc, float(temperature),
+                                      ptr(A), stream_handle(dev)))
+    return A
+
+
+def _ancestors(params):
+    torch = _torch()
+    anc = params["ancestors"]
+    if isinstance(anc, (list, tuple)):
+        anc = torch.stack([torch.as_tensor(a) for a in anc])
+    return _dev(anc)
+
+
+def update_seq(params, sequences, temperature: float = 1.0):
+    """S[n_leaf:] = softmax(ancestors * T) (tree.py:127-130)."""
+    anc = _ancestors(params)
+    S = _dev(sequences, anc.device).clone()
+    n_leaf = (S.shape[0] + 1) // 2
+    n_anc, L, Q = anc.shape
+    if S.shape[0] - n_leaf != n_anc or tuple(S.shape[1:]) != (L, Q):
+        raise ValueError("ancestors must be (n_nodes - (n_nodes+1)//2, L, Q)")
+    check(lib().trex_tree_update_seq(ptr(anc), n_anc, L, Q, float(temperature), ptr(S[n_leaf:]),
+                                     stream_handle(S.device)))
+    return S
+
+
+def enforce_graph_constraints(adjacency, scaling_factor: float):
+    """scale * sum_cols (sum_rows A[:-1, -n_anc:] - 2)^2 (tree.py:156-160)."""
+    torch = _torch()
+    A = _dev(adjacency)
+    out = torch.empty((1,), dtype=torch.float32, device=A.device)
+    ws = _workspace(A.shape[0], 1, A.device)
+    check(lib().trex_tree_constraint(ptr(A), A.shape[0], float(scaling_factor), 1.0, ptr(out), 0,
+                                     None, ptr(ws), stream_handle(A.device)))
+    return out[0]
+
+
+# ---------------------------------------------------------------------------
+# tree costs
+# ---------------------------------------------------------------------------
+def compute_surrogate_cost(sequences, adjacency):
+    """0.5 * sum_ij A_ij ||S_i - S_j||^2 (tree.py:163-209)."""
+    torch = _torch()
+    S = _dev(sequences)
+    A = _dev(adjacency, S.device)
+    N = S.shape[0]
+    K = S[0].numel()
+    out = torch.empty((1,), dtype=torch.float32, device=S.device)
+    ws = _workspace(N, K, S.device)
+    check(lib().trex_tree_surrogate(ptr(S), ptr(A), N, K, ptr(out), None, None, None, ptr(ws),
+                                    ws.numel(), stream_handle(S.device)))
+    return out[0]
+
+
+def surrogate_cost_and_grads(sequences, adjacency):
+    """(cost, dS, dA) of compute_surrogate_cost: dS = (diag(r+c) - (A+A^T)) S,
+    dA = (E_i + E_j)/2 - G_ij."""
+    torch = _torch()
+    S = _dev(sequences)
+    A = _dev(adjacency, S.device)
+    N = S.shape[0]
+    K = S[0].numel()
+    out = torch.empty((1,), dtype=torch.float32, device=S.device)
+    dS = torch.empty_like(S)
+    dA = torch.empty_like(A)
+    ws = _workspace(N, K, S.device)
+    check(lib().trex_tree_surrogate(ptr(S), ptr(A), N, K, ptr(out), ptr(dS), ptr(dA), None,
+                                    ptr(ws), ws.numel(), stream_handle(S.device)))
+    return out[0], dS, dA
+
+
+def compute_soft_cost(sequences, adjacency, cost_matrix=None):
+    """Weighted variant (tree.py:212-266): C None, (Q,) diagonal or (Q, Q)."""
+    torch = _torch()
+    S = _dev(sequences)
+    A = _dev(adjacency, S.device)
+    N, L, Q = S.shape
+    ckind = 0
+    C = None
+    W = None
+    if cost_matrix is not None:
+        C = _dev(cost_matrix, S.device)
+        ckind = 1 if C.ndim == 1 else 2
+        W = torch.empty_like(S)
+    out = torch.empty((1,), dtype=torch.float32, device=S.device)
+    ws = _workspace(N, L * Q, S.device)
+    check(lib().trex_tree_soft_cost(ptr(S), ptr(A), ptr(C), ckind, N, L, Q, ptr(out), ptr(W),
+                                    ptr(ws), ws.numel(), stream_handle(S.device)))
+    return out[0]
+
+
+def compute_cost(sequences, adjacency, substitution_matrix):
+    """Exact cost of a labelled tree (tree.py:286-296)."""
+    torch = _torch()
+    S = _dev(sequences)
+    A = _dev(adjacency, S.device)
+    C = _dev(substitution_matrix, S.device)
+    N, L, Q = S.shape
+    out = torch.empty((1,), dtype=torch.float32, device=S.device)
+    ws = _workspace(N, 1, S.device)
+    check(lib().trex_tree_compute_cost(ptr(S), ptr(A), ptr(C), N, L, Q, ptr(out), ptr(ws),
+                                       stream_handle(S.device)))
+    return out[0]
+
+
+# ---------------------------------------------------------------------------
+# loss and its gradient
+# ---------------------------------------------------------------------------
+def loss_and_grad(noise, params, sequences, temperature: float, adjacency=None, *,
+                  graph_constraint_scale: float = 10.0, fix_seqs: bool = False,
+                  fix_tree: bool = False):
+    """compute_loss (tree.py:336-342) and d loss / d params.
+
+    update_tree runs at temperature 1.0: compute_loss does not pass T to it
+    (tree.py:338).  Returns (loss, {"tree_params", "ancestors"}).
+    """
+    torch = _torch()
+    theta = _dev(params["tree_params"])
+    anc = _ancestors(params)
+    dev = theta.device
+    st = stream_handle(dev)
+    S = _dev(sequences, dev) if fix_seqs else update_seq({"ancestors": anc}, sequences,
+                                                         temperature)
+    A = _dev(adjacency, dev) if fix_tree else update_tree(noise, {"tree_params": theta}, 1.0)
+    N = S.shape[0]
+    K = S[0].numel()
+    loss = torch.empty((1,), dtype=torch.float32, device=dev)
+    dS = torch.empty_like(S)
+    dA = torch.empty_like(A)
+    ws = _workspace(N, K, dev)
+    check(lib().trex_tree_surrogate(ptr(S), ptr(A), N, K, ptr(loss), ptr(dS), ptr(dA), None,
+                                    ptr(ws), ws.numel(), st))
+    # + T * constraint (value and gradient accumulated into dA)
+    check(lib().trex_tree_constraint(ptr(A), N, float(graph_constraint_scale),
+                                     float(temperature), ptr(loss), 1, ptr(dA), ptr(ws), st))
+    grads = {"tree_params": torch.zeros_like(theta), "ancestors": torch.zeros_like(anc)}
+    if not fix_tree and theta.shape[1] > 0:
+        check(lib().trex_tree_update_tree_bwd(ptr(A), ptr(dA), None, N, theta.shape[1], 1.0,
+                                              ptr(grads["tree_params"]), st))
+    if not fix_seqs:
+        n_leaf = (N + 1) // 2
+        n_anc, L, Q = anc.shape
+        check(lib().trex_tree_update_seq_bwd(ptr(S[n_leaf:]), ptr(dS[n_leaf:]), n_anc, L, Q,
+                                             float(temperature), ptr(grads["ancestors"]), st))
+    return loss[0], grads
+
+
+def compute_loss(noise, params, sequences, _metadata, temperature: float, adjacency, *,
+                 graph_constraint_scale: float = 10.0, verbose: bool = False,
+                 fix_seqs: bool = False, fix_tree: bool = False):
+    """Total loss (tree.py:299-361); ``noise`` replaces the PRNG key."""
+    loss, _ = loss_and_grad(noise, params, sequences, temperature, adjacency,
+                            graph_constraint_scale=graph_constraint_scale, fix_seqs=fix_seqs,
+                            fix_tree=fix_tree)
+    return loss
+
+
+# ---------------------------------------------------------------------------
+# optimiser (optax semantics)
+# ---------------------------------------------------------------------------
+class Adam:
+    """optax.adam(lr, b1, b2, eps) [chained after clip_by_global_norm(clip)].
+
+    Updates the parameter tensors in place with one fused kernel per tensor.
+    """
+
+    def __init__(self, params: dict, lr: float, b1=0.9, b2=0.999, eps=1e-8, clip_norm=None):
+        torch = _torch()
+        self.lr, self.b1, self.b2, self.eps, self.clip = lr, b1, b2, eps, clip_norm
+        self.mu = {k: torch.zeros_like(v) for k, v in params.items()}
+        self.nu = {k: torch.zeros_like(v) for k, v in params.items()}
+        self.count = 0
+        dev = next(iter(params.values())).device
+        self.parts = torch.zeros(512 * max(1, len(params)), dtype=torch.float64, device=dev)
+
+    def step(self, params: dict, grads: dict):
+        self.count += 1
+        st = stream_handle(next(iter(params.values())).device)
+        keys = sorted(params)
+        nparts = 0
+        if self.clip is not None:
+            for i, k in enumerate(keys):
+                check(lib().trex_sq_norm_parts(ptr(grads[k]), grads[k].numel(),
+                                               ptr(self.parts[512 * i:]), 512, st))
+            nparts = 512 * len(keys)
+        for k in keys:
+            p, g = params[k], grads[k]
+            if not (p.is_contiguous() and g.is_contiguous()):
+                raise ValueError("params and grads must be contiguous")
+            check(lib().trex_adam_step(ptr(p), ptr(g), ptr(self.mu[k]), ptr(self.nu[k]),
+                                       p.numel(), self.count, float(self.lr), float(self.b1),
+                                       float(self.b2), float(self.eps),
+                                       ptr(self.parts) if nparts else None, nparts,
+                                       float(self.clip or 0.0), st))
