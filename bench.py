@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly, no hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 single-tree line")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 tree-cost loop line")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/pmc_traffic.py)")
@@ -151,6 +152,48 @@ def c2_line(torch, device, args, cpu_threads):
     out["cpu_port_ms"] = cpu_s * 1e3
     out["speedup_vs_cpu_port"] = cpu_s / gpu_s
     return out
+
+
+def c5_line(torch, device, steps=20, warmup=3):
+    """C5 (BASELINE.json configs[4]) on one GPU: 256 taxa (511 nodes) x 50 000
+    sites x 4 states, joint Adam optimisation step (update_seq, update_tree,
+    surrogate + graph constraint, their VJPs, optax Adam) -- trex's
+    tests/test_convergence.py:208-261 loop at C5 size.  Eager launches (Adam's
+    bias correction changes every step)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cases import simulate_leaves
+
+    from trex_amd.tree import TreeOptimizer
+
+    nl, L, Q = 256, 50000, 4
+    n = 2 * nl - 1
+    seqs, _ = simulate_leaves(nl, L, Q, 5, seed=6)
+    S = torch.zeros((n, L, Q), dtype=torch.float32, device=device)
+    S[:nl] = torch.nn.functional.one_hot(torch.as_tensor(seqs[:nl].astype(np.int64),
+                                                         device=device), Q).float()
+    g = torch.Generator(device=device)
+    g.manual_seed(7)
+    params = {"tree_params": torch.randn((n - 1, nl - 1), generator=g, device=device),
+              "ancestors": torch.randn((nl - 1, L, Q), generator=g, device=device)}
+    from trex_amd.tree import gumbel_noise
+
+    noise = [gumbel_noise((n - 1, nl - 1), generator=g, device=device) for _ in range(4)]
+    opt = TreeOptimizer(S, params, lr=0.01)
+    for k in range(warmup):
+        opt.step(max(0.1, 2.0 * (1.0 - k / 5000)), noise[k % 4])
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for k in range(steps):
+        loss = opt.step(max(0.1, 2.0 * (1.0 - (warmup + k) / 5000)), noise[k % 4])
+    ev1.record()
+    torch.cuda.synchronize()
+    sec = ev0.elapsed_time(ev1) * 1e-3 / steps
+    flops = 4.0 * n * n * L * Q  # G = S S^T and dS = M S, as trex's GEMMs
+    return {"workload": "C5: 511-node relaxed tree x 50000 sites x 4 states, joint Adam step "
+                        "(surrogate + constraint + VJPs + optax adam), f32 MFMA GEMMs",
+            "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec,
+            "gemm_tflops": flops / sec / 1e12, "loss_last": float(loss)}
 
 
 def cpu_baseline(ch, leaves_np, cost_np, tau, L, n, Q, threads):
@@ -307,6 +350,8 @@ def main():
                                                   tau, L, n, Q, threads)
         if not args.no_c2:
             result["c2"] = c2_line(torch, device, args, threads)
+        if not args.no_c5:
+            result["c5"] = c5_line(torch, device)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

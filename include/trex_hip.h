@@ -181,6 +181,15 @@ int trex_tree_surrogate(const float* S, const float* A, int N, int64_t K, float*
                         float* dS, float* dA, float* G_out, void* workspace,
                         int64_t workspace_bytes, void* stream);
 
+/* The surrogate in phases (site-sharded data parallelism all-reduces the
+ * N x N Gram matrix between the first two):  G = S S^T;  loss / dA / M =
+ * diag(r+c) - (A+A^T) from (A, G);  dS = M S.  Workspace for combine: >= 8*N B. */
+int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
+                   int64_t workspace_bytes, void* stream);
+int trex_tree_surrogate_combine(const float* A, const float* G, int N, float* loss, float* dA,
+                                float* M, void* workspace, void* stream);
+int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS, void* stream);
+
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */
 int trex_tree_soft_cost(const float* S, const float* A, const float* C, int ckind, int N, int L,

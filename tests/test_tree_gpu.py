@@ -187,3 +187,22 @@ def test_c5_scale_gram_properties(device):
     i, j = 3, parent[3]
     agree = int((seq[i] == seq[j]).sum())
     assert float(dA1[i, j]) == L - agree
+
+
+def test_tree_optimizer_matches_oracle_loop(device):
+    """The fused device loop == oracle compute_loss + adam, step by step."""
+    params, noise, seqs = _tree_case(16, 50, 4, 17)
+    opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                          lr=0.01)
+    p_ref = {k: v.astype(np.float64) for k, v in params.items()}
+    st = T.adam_init(p_ref)
+    nz = _t(noise, device)
+    for step in range(6):
+        Tt = max(0.1, 2.0 * (1.0 - step / 50))
+        loss = opt.step(Tt, nz)
+        rloss, gr = T.compute_loss(noise, p_ref, seqs, Tt, None)
+        np.testing.assert_allclose(float(loss), rloss, rtol=RTOL)
+        upd, st = T.adam_update(gr, st, lr=0.01)
+        p_ref = {k: p_ref[k] + upd[k] for k in p_ref}
+    for k in p_ref:
+        np.testing.assert_allclose(_n(opt.params[k]), p_ref[k], rtol=5e-5, atol=5e-6)

@@ -799,3 +799,38 @@ extern "C" int trex_tree_discretize(const float* A, int nrows, int ncols, int n_
                      n_nodes, out);
   return tree_hip_check("trex_tree_discretize");
 }
+
+// ---- split surrogate phases (for site-sharded multi-GPU: all-reduce G between
+// trex_tree_gram and trex_tree_surrogate_combine) ----
+extern "C" int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
+                              int64_t workspace_bytes, void* stream) {
+  if (!S || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF)
+    return set_error(TREX_E_ARG, "trex_tree_gram: bad arguments");
+  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
+    return set_error(TREX_E_ARG, "trex_tree_gram: workspace too small");
+  return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream);
+}
+
+extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N, float* loss,
+                                           float* dA, float* M, void* workspace, void* stream) {
+  if (!A || !G || !loss || !workspace || N <= 0)
+    return set_error(TREX_E_ARG, "trex_tree_surrogate_combine: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  double* rowloss = static_cast<double*>(workspace);
+  hipLaunchKernelGGL(surrogate_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, dA, M,
+                     rowloss);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0);
+  return tree_hip_check("trex_tree_surrogate_combine");
+}
+
+extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,
+                            void* stream) {
+  if (!M || !S || !dS || N <= 0 || K <= 0 || K > 0x7FFFFFFF)
+    return set_error(TREX_E_ARG, "trex_tree_mf: bad arguments");
+  const int nrowt = (N + 63) / 64;
+  const int ncolb = (int)((K + 63) / 64);
+  const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
+  hipLaunchKernelGGL(mf_kernel, dim3(blocks), dim3(kWave), 0, (hipStream_t)stream, M, S, N,
+                     (int)K, nrowt, ncolb, dS);
+  return tree_hip_check("trex_tree_mf");
+}

@@ -275,3 +275,76 @@ class Adam:
                                        float(self.b2), float(self.eps),
                                        ptr(self.parts) if nparts else None, nparts,
                                        float(self.clip or 0.0), st))
+
+
+class TreeOptimizer:
+    """Device-resident compute_loss + optax-Adam step: the C5 loop.
+
+    Joint optimisation of tree_params and ancestor logits as in
+    tests/test_convergence.py:208-261 (loss = surrogate(update_seq(params, T),
+    update_tree(params, 1.0)) + T * constraint, Adam(lr)).  Buffers are
+    allocated once; ``step`` launches only HIP kernels (graph-capturable).
+
+    Site sharding (``group``): each rank holds a contiguous block of sites
+    (its leaf one-hot rows and ancestor logits for those sites).  The only
+    exchange is an all-reduce of the N x N Gram matrix; every rank then
+    computes the same loss, dA and tree_params update, and updates its own
+    ancestor logits.
+    """
+
+    def __init__(self, sequences, params: dict, lr: float = 0.01, *,
+                 graph_constraint_scale: float = 10.0, clip_norm=None, group=None):
+        torch = _torch()
+        self.S = _dev(sequences).clone()  # (N, L, Q): leaf rows fixed, ancestors overwritten
+        dev = self.S.device
+        self.params = {"tree_params": _dev(params["tree_params"], dev).clone(),
+                       "ancestors": _ancestors(params).to(dev).clone()}
+        self.N, self.L, self.Q = self.S.shape
+        self.K = self.L * self.Q
+        self.n_leaf = (self.N + 1) // 2
+        self.n_anc = self.N - self.n_leaf
+        self.scale = float(graph_constraint_scale)
+        self.group = group
+        if group is not None and clip_norm is not None:
+            raise NotImplementedError("clip_by_global_norm with site sharding")
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.A = torch.empty((self.N, self.N), **f32)
+        self.G = torch.empty((self.N, self.N), **f32)
+        self.M = torch.empty((self.N, self.N), **f32)
+        self.dA = torch.empty((self.N, self.N), **f32)
+        self.dS = torch.empty_like(self.S)
+        self.loss = torch.zeros((1,), **f32)
+        self.grads = {k: torch.zeros_like(v) for k, v in self.params.items()}
+        self.ws = torch.empty(int(lib().trex_tree_workspace_bytes(self.N, self.K)),
+                              dtype=torch.uint8, device=dev)
+        self.opt = Adam(self.params, lr, clip_norm=clip_norm)
+
+    def step(self, temperature: float, noise):
+        """One optimisation step; returns the (device) loss before the update."""
+        L_ = lib()
+        st = stream_handle(self.S.device)
+        T = float(temperature)
+        p = self.params
+        N, K = self.N, self.K
+        check(L_.trex_tree_update_seq(ptr(p["ancestors"]), self.n_anc, self.L, self.Q, T,
+                                      ptr(self.S[self.n_leaf:]), st))
+        check(L_.trex_tree_update_tree(ptr(p["tree_params"]), ptr(noise), None, N, self.n_anc,
+                                       1.0, ptr(self.A), st))
+        check(L_.trex_tree_gram(ptr(self.S), N, K, ptr(self.G), ptr(self.ws), self.ws.numel(),
+                                st))
+        if self.group is not None:
+            import torch.distributed as dist
+
+            dist.all_reduce(self.G, group=self.group)
+        check(L_.trex_tree_surrogate_combine(ptr(self.A), ptr(self.G), N, ptr(self.loss),
+                                             ptr(self.dA), ptr(self.M), ptr(self.ws), st))
+        check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
+                                      ptr(self.dA), ptr(self.ws), st))
+        check(L_.trex_tree_mf(ptr(self.M), ptr(self.S), N, K, ptr(self.dS), st))
+        check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc, 1.0,
+                                           ptr(self.grads["tree_params"]), st))
+        check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]), ptr(self.dS[self.n_leaf:]),
+                                          self.n_anc, self.L, self.Q, T,
+                                          ptr(self.grads["ancestors"]), st))
+        self.opt.step(self.params, self.grads)
+        return self.loss
