@@ -83,8 +83,12 @@ int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
  *            sankoff.py:50)
  *   cost     fp32  [Q][Q]            substitution cost C[parent][child]
  *   tau      0 => hard min-plus (trex); >0 => softmin relaxation
- *   dp       fp32  [B][n_int][Q][L]  internal rows (required)
+ *   dp       fp32  internal rows (required), layout by Q:
+ *            Q <= 4: [B][n_int][Q][L]  (sites innermost; lane-per-site kernels)
+ *            4 < Q <= 32: [B][n_int][L][Q]  (site-major; lane-per-state
+ *            kernels, e.g. protein Q = 20) -- see trex_dp_site_major
  *   site_score fp32 [B][L] or NULL;  tree_score fp32 [B] (required)
+ * Q > 32 returns TREX_E_UNSUPPORTED.
  * ---------------------------------------------------------------------- */
 int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
                      const float* cost, int B, int L, int n_all, int Q, float tau,
@@ -97,10 +101,10 @@ int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
  * w.r.t. the cost matrix -- what jax.grad of run_sankoff's total
  * (sankoff.py:187) w.r.t. cost_matrix computes for tau=0 (tie-averaged min
  * subgradient), and the softmin adjoint for tau>0.
- *   dp         fp32 [B][n_int][Q][L] from trex_sankoff_fwd (same tau)
+ *   dp         fp32 DP table from trex_sankoff_fwd (same tau, same layout)
  *   d_tree_score fp32 [B] or NULL (= all ones)
  *   d_cost     fp32 [Q][Q] out (summed over trees, deterministic)
- *   marginals  fp32 [B][n_int][Q][L] or NULL: dScore/dD_v (soft ancestral
+ *   marginals  fp32, dp's layout, or NULL: dScore/dD_v (soft ancestral
  *              state posteriors for tau>0)
  *   anc_states int8 [B][n_int][L] or NULL: argmax_i marginals (first index)
  * ---------------------------------------------------------------------- */
@@ -130,7 +134,7 @@ int trex_sankoff_fwd_bwd(const int32_t* plan, int n_slots, const int8_t* leaves,
  * reference's DFS (backtrack_sankoff_jit, sankoff.py:191-267) re-deriving
  * each child's state as the first argmin of C[s_parent] + D_child
  * (sankoff.py:67-69) instead of storing the backtracking table.
- *   dp         fp32 [B][n_int][Q][L] from a tau=0 forward
+ *   dp         fp32 DP table (either layout) from a tau=0 forward
  *   anc_states int8 [B][n_int][L] out (0 for nodes the DFS never reaches)
  * ---------------------------------------------------------------------- */
 int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, const float* cost,
@@ -145,6 +149,10 @@ int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, const float* c
  * ---------------------------------------------------------------------- */
 int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,
                            int n_all, int Q, float* out, void* stream);
+
+/* 1 when the DP / marginal tables for Q states are site-major
+ * [B][n_int][L][Q], 0 when they are [B][n_int][Q][L]. */
+int trex_dp_site_major(int Q);
 
 /* ========================================================================
  * Tree-cost path (src/trex/tree.py).  N = n_nodes, S = soft sequences

@@ -1,0 +1,212 @@
+"""GPU parity of the Q > 4 (lane-per-state) Sankoff kernels vs the CPU oracle.
+
+Same bars as tests/test_sankoff_gpu.py: hard DP table / totals / ancestral
+states bit-exact, hard gradient rtol 1e-6, softmin score / gradient /
+marginals rtol 1e-5 vs the fp64 oracle.  Q > 4 tables are site-major
+([B][n_int][L][Q], trex_hip.h), so oracle tables are transposed to compare.
+Q = 20 is the protein alphabet of BASELINE config C3; 5, 13, 21 and 32
+exercise the padded-state groups (G = 8, 16, 32).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from _cases import hamming, int_cost, random_leaves, random_topologies
+from oracle.sankoff_ref import run_sankoff_ref
+from oracle.softmin_ref import batched_fwd_bwd_ref
+from trex_amd import SankoffEngine, TreePlan, run_sankoff
+from trex_amd.topology import adjacency_from_children
+
+pytestmark = pytest.mark.gpu
+
+SOFT_RTOL = 1e-5
+
+
+def _engine(children, L, Q, device):
+    return SankoffEngine(TreePlan(children), L, Q, device)
+
+
+def _dev(x, device, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(device).contiguous()
+
+
+def _sm(t):
+    """engine site-major table (B, n_int, L, Q) -> oracle layout (B, n_int, Q, L)."""
+    return t.cpu().numpy().transpose(0, 1, 3, 2)
+
+
+def test_site_major_layout_flag(device):
+    eng = _engine(random_topologies(1, 4, seed=0), 10, 20, device)
+    assert eng.site_major and eng.dp_shape == (1, 3, 10, 20)
+    eng4 = _engine(random_topologies(1, 4, seed=0), 10, 4, device)
+    assert not eng4.site_major
+
+
+@pytest.mark.parametrize("Q", [5, 20, 21])
+@pytest.mark.parametrize("L", [1, 7, 130, 1000])
+def test_run_sankoff_bitexact_wide(device, Q, L):
+    ch = random_topologies(1, 16, seed=200 + L + Q)[0]
+    adj = adjacency_from_children(ch)[0]
+    rng = np.random.default_rng(L * 3 + Q)
+    seqs = rng.integers(0, Q, size=(16, L)).astype(np.float32)
+    cost = int_cost(Q, seed=Q + L)
+    recon, dp, total = run_sankoff(adj, cost, seqs, 31, Q, 16, return_path=True, device=device)
+    r_recon, r_dp, r_total = run_sankoff_ref(adj, cost, seqs, 31, Q, 16, return_path=True)
+    np.testing.assert_array_equal(dp.cpu().numpy(), r_dp)
+    np.testing.assert_array_equal(recon.cpu().numpy(), r_recon)
+    assert float(total) == float(r_total)
+
+
+@pytest.mark.parametrize("L,Q,n", [(1, 20, 8), (300, 20, 16), (1000, 20, 64), (777, 5, 12),
+                                   (513, 13, 20), (200, 32, 10), (64, 21, 9)])
+def test_batched_hard_fwd_grad_wide(device, L, Q, n):
+    B = 4
+    ch = random_topologies(B, n, seed=L + n + Q)
+    leaves = random_leaves(B, n, L, Q, seed=L + Q, missing=0.05)
+    cost = int_cost(Q, seed=L + 1)
+    dts_np = np.arange(1, B + 1) / B
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, 0.0, d_tree_score=dts_np)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    f = eng.forward(lv, c, 0.0, dp=True, site_score=True)
+    np.testing.assert_array_equal(_sm(f.dp), ref["dp"].astype(np.float32))
+    np.testing.assert_array_equal(f.site_score.cpu().numpy(),
+                                  ref["site_score"].astype(np.float32))
+    np.testing.assert_array_equal(f.tree_score.cpu().numpy(), ref["tree_score"].astype(np.float32))
+    dts = torch.as_tensor(dts_np, dtype=torch.float32, device=device)
+    dc, mg, _ = eng.backward(lv, c, 0.0, f.dp, dts, marginals=True)
+    np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(_sm(mg), ref["marginals"], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("Q", [20, 7])
+def test_backtrack_wide_matches_reference(device, Q):
+    B, n, L = 3, 24, 515
+    ch = random_topologies(B, n, seed=3 + Q)
+    leaves = random_leaves(B, n, L, Q, seed=4 + Q)
+    cost = int_cost(Q, seed=5)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    f = eng.forward(lv, c, 0.0)
+    anc = eng.backtrack(c, f.dp).cpu().numpy()
+    adj = adjacency_from_children(ch)
+    for b in range(B):
+        r = run_sankoff_ref(adj[b], cost, leaves[b].astype(np.float32), 2 * n - 1, Q, n,
+                            return_path=True)
+        np.testing.assert_array_equal(anc[b].astype(np.float32), r[0][n:])
+
+
+@pytest.mark.parametrize("tau", [1.0, 0.5, 0.1])
+@pytest.mark.parametrize("L,n,Q", [(100, 8, 20), (1000, 64, 20), (301, 16, 6), (257, 12, 32)])
+def test_softmin_fwd_grad_wide_vs_fp64(device, tau, L, n, Q):
+    B = 2
+    ch = random_topologies(B, n, seed=n + 13)
+    leaves = random_leaves(B, n, L, Q, seed=L + 5)
+    cost = hamming(Q)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    f = eng.forward(lv, c, tau, dp=True, site_score=True)
+    np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
+    np.testing.assert_allclose(f.site_score.cpu().numpy(), ref["site_score"], rtol=SOFT_RTOL,
+                               atol=1e-5)
+    dc, mg, anc = eng.backward(lv, c, tau, f.dp, marginals=True, anc_states=True)
+    np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL,
+                               atol=SOFT_RTOL * np.abs(ref["d_cost"]).max())
+    mtol = max(2e-5, 8 * 1.2e-7 * np.abs(ref["dp"]).max() / tau)
+    np.testing.assert_allclose(_sm(mg), ref["marginals"], atol=mtol)
+    m = ref["marginals"]
+    top2 = np.sort(m, axis=2)[:, :, -2:, :]
+    clear = (top2[:, :, 1] - top2[:, :, 0]) > 4 * mtol
+    np.testing.assert_array_equal(anc.cpu().numpy()[clear], m.argmax(axis=2)[clear])
+
+
+def test_softmin_wide_direct_path_and_hard_root(device):
+    """range(C) > 40 tau selects the per-row stabilised softmin; hard_root
+    scores the root with a hard min."""
+    B, n, L, Q = 2, 16, 200, 20
+    ch = random_topologies(B, n, seed=1)
+    leaves = random_leaves(B, n, L, Q, seed=2)
+    cost = int_cost(Q, seed=3, lo=1, hi=9)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    for tau, hard_root in ((0.05, False), (0.3, True)):
+        ref = batched_fwd_bwd_ref(ch, leaves, cost, tau, hard_root=hard_root)
+        f = eng.forward(lv, c, tau, hard_root=hard_root)
+        np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"],
+                                   rtol=SOFT_RTOL)
+        dc, _, _ = eng.backward(lv, c, tau, f.dp, hard_root=hard_root)
+        np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL,
+                                   atol=SOFT_RTOL * np.abs(ref["d_cost"]).max())
+
+
+def test_softmin_wide_missing_leaves(device):
+    B, n, L, Q, tau = 2, 8, 100, 20, 1.0
+    ch = random_topologies(B, n, seed=19)
+    leaves = random_leaves(B, n, L, Q, seed=103, missing=0.03)
+    cost = hamming(Q)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
+    eng = _engine(ch, L, Q, device)
+    f = eng.forward(_dev(leaves, device), _dev(cost, device, torch.float32), tau)
+    np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
+    dc, _, _ = eng.backward(_dev(leaves, device), _dev(cost, device, torch.float32), tau, f.dp)
+    np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=2e-3)
+
+
+@pytest.mark.parametrize("tau", [0.0, 0.5])
+def test_fused_equals_separate_wide(device, tau):
+    B, n, L, Q = 3, 20, 999, 20
+    ch = random_topologies(B, n, seed=21)
+    leaves = random_leaves(B, n, L, Q, seed=22, missing=0.01)
+    cost = int_cost(Q, seed=23)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    dts = torch.linspace(0.5, 2.0, B, device=device)
+    f, dc, mg, an = eng.fwd_bwd(lv, c, tau, dts, site_score=True, marginals=True,
+                                anc_states=True)
+    f2 = eng.forward(lv, c, tau, site_score=True)
+    dc2, mg2, an2 = eng.backward(lv, c, tau, f2.dp, dts, marginals=True, anc_states=True)
+    assert torch.equal(f.dp, f2.dp)
+    assert torch.equal(f.tree_score, f2.tree_score)
+    assert torch.equal(f.site_score, f2.site_score)
+    assert torch.equal(dc, dc2) and torch.equal(mg, mg2) and torch.equal(an, an2)
+
+
+def test_c3_scale_properties(device):
+    """C3 shape: 64 taxa x 10 000 sites x 20 states, softmin (tau 0.5) +
+    ancestral reconstruction.  Score and dC vs the fp64 oracle, determinism,
+    tau = 0 ancestral states bit-exact vs the reference backtrack."""
+    n, L, Q, tau = 64, 10000, 20, 0.5
+    ch = random_topologies(1, n, seed=31)
+    leaves = random_leaves(1, n, L, Q, seed=32)
+    cost = int_cost(Q, seed=3)
+    eng = _engine(ch, L, Q, device)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    f, dc, mg, an = eng.fwd_bwd(lv, c, tau, marginals=True, anc_states=True)
+    f2, dc2, mg2, an2 = eng.fwd_bwd(lv, c, tau, marginals=True, anc_states=True)
+    assert torch.equal(f.tree_score, f2.tree_score) and torch.equal(dc, dc2)
+    assert torch.equal(mg, mg2) and torch.equal(an, an2)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
+    np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
+    np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL,
+                               atol=SOFT_RTOL * np.abs(ref["d_cost"]).max())
+    # hard path + trex backtrack at full size
+    h = eng.forward(lv, c, 0.0)
+    anc = eng.backtrack(c, h.dp).cpu().numpy()[0]
+    adj = adjacency_from_children(ch)[0]
+    r = run_sankoff_ref(adj, cost, leaves[0].astype(np.float32), 2 * n - 1, Q, n,
+                        return_path=True)
+    assert float(h.tree_score[0]) == float(r[2])
+    np.testing.assert_array_equal(anc.astype(np.float32), r[0][n:])

@@ -44,6 +44,7 @@ SIGNATURES = {
                                     _p, _p, _p, _p, _p, _p, _p, _p, _c_i64, _p]),
     "trex_sankoff_backtrack": (_c_i, [_p, _c_i, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
     "trex_dp_to_trex_layout": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
+    "trex_dp_site_major": (_c_i, [_c_i]),
     # tree-cost path
     "trex_tree_discretize": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _p]),
     "trex_tree_update_seq": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _p, _p]),

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <string>
 
+#include "sankoff_dev.h"
 #include "trex_common.h"
 
 namespace trex {
@@ -25,9 +26,6 @@ namespace {
 
 thread_local char g_err[512] = "no error";
 
-constexpr float kSentinel = 1e5f;  // sankoff.py:152
-constexpr int kWave = 64;
-constexpr int kKindLeaf = 1, kKindInt = 2;  // 0 = 1e5 sentinel row
 
 // --------------------------------------------------------------------------
 // per-lane vector helpers (SPT consecutive sites per lane)
@@ -85,36 +83,11 @@ __device__ __forceinline__ void st_codes(int8_t* __restrict__ p, const int (&c)[
   }
 }
 
-// Read-only, wave-uniform data (topology program, cost matrix) goes through
-// the constant address space so hipcc emits scalar loads (s_load): vector
-// loads would be ordered behind the wave's in-flight DP-table stores in vmcnt.
-template <class T>
-using cptr = const __attribute__((address_space(4))) T*;
-template <class T>
-__device__ __forceinline__ cptr<T> as_const(const T* p) {
-  return (cptr<T>)(p);
-}
-
-struct I4 {
-  int x, y, z, w;
-};
-__device__ __forceinline__ I4 load_step(cptr<int> prog, int k) {
-  return I4{prog[4 * k], prog[4 * k + 1], prog[4 * k + 2], prog[4 * k + 3]};
-}
-
-__device__ __forceinline__ float uniform(float x) {
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
-}
-
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
-
 // --------------------------------------------------------------------------
 // cost matrix in SGPRs.  MODE: kHard (min-plus), kSoftK (factored softmin,
 // K[i][j] = exp(-(C[i][j]-cmin)/tau) in SGPRs), kSoftDirect (per-row
 // stabilised softmin, used when range(C)/tau > 40 would underflow K).
 // --------------------------------------------------------------------------
-constexpr int kHard = 0, kSoftK = 1, kSoftDirect = 2;
 
 template <int Q>
 struct Coef {
@@ -123,10 +96,6 @@ struct Coef {
   float cmin;
 };
 
-// range(C)/tau <= 40: the factored form keeps every K >= e^-40
-__device__ __forceinline__ bool use_ktrick(float cmin, float cmax, float a) {
-  return (cmax - cmin) * a <= 57.70780f;  // log2(e^40)
-}
 
 template <int Q>
 __device__ __forceinline__ void cost_range(const float* __restrict__ cost_, float& cmin,
@@ -251,14 +220,6 @@ __device__ __forceinline__ float pick(const float (&row)[Q], int code) {
   return (code & 2) ? hi : lo;
 }
 
-// ---- buffer (SRD) access: 32-bit lane offset in voffset, row offset in
-// soffset, no 64-bit VALU address arithmetic per access ----
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
 
 template <int SPT>
 __device__ __forceinline__ void bst(rsrc_t r, int voff, int soff, const float (&o)[SPT]) {
@@ -462,11 +423,6 @@ __device__ __forceinline__ void root_score(const float (&d)[Q][SPT], float a, fl
   }
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
-}
 
 // --------------------------------------------------------------------------
 // Unified Sankoff kernel: PHASE 1 = forward, 2 = adjoint, 3 = both (fused).
@@ -498,19 +454,6 @@ struct KArgs {
   int* counters;        // [B+1], zero at rest (self-resetting)
 };
 
-__device__ __forceinline__ void store_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_sc1(const double* p) {
-  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// sum of n values (lane-strided, fixed order) -> every lane
-__device__ __forceinline__ double wave_sum_strided(const double* p, int n, int lane) {
-  double v = 0.0;
-  for (int t = lane; t < n; t += kWave) v += load_sc1(p + t);
-  return wave_sum(v);
-}
 
 // LDS map (floats): [0, 64) leaf tables: T[code][i] (message; code Q =
 // missing leaf) at 0, IK[code][i] = 1/K[i][code] (factored-form leaf adjoint
@@ -963,7 +906,7 @@ __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
   }
 }
 
-// dp [B][n_int][Q][L] -> trex VmappedDPTable [B][L][n_all][Q]
+// dp [B][n_int][Q][L] (Q <= 4) / [B][n_int][L][Q] (Q > 4) -> trex VmappedDPTable [B][L][n_all][Q]
 __global__ __launch_bounds__(256) void to_trex_layout_kernel(const float* __restrict__ dp,
                                                             const int8_t* __restrict__ leaves,
                                                             int B, int L, int n_all, int nl, int Q,
@@ -981,8 +924,13 @@ __global__ __launch_bounds__(256) void to_trex_layout_kernel(const float* __rest
       const int code = leaves[((size_t)b * nl + node) * L + l];
       for (int q = 0; q < Q; ++q) o[q] = (code == q) ? 0.0f : kSentinel;
     } else {
-      const float* src = dp + (((size_t)b * ni + (node - nl)) * Q) * L + l;
-      for (int q = 0; q < Q; ++q) o[q] = src[(size_t)q * L];
+      if (Q > 4) {  // site-major [B][n_int][L][Q]
+        const float* src = dp + (((size_t)b * ni + (node - nl)) * L + l) * Q;
+        for (int q = 0; q < Q; ++q) o[q] = src[q];
+      } else {
+        const float* src = dp + (((size_t)b * ni + (node - nl)) * Q) * L + l;
+        for (int q = 0; q < Q; ++q) o[q] = src[(size_t)q * L];
+      }
     }
   }
 }
@@ -997,8 +945,9 @@ struct Shape {
 int check_shape(const char* fn, int B, int L, int n_all, int Q, Shape* sh) {
   if (B <= 0 || L <= 0 || n_all < 3 || n_all > 65535 || Q < 2)
     return set_error(TREX_E_ARG, "%s: bad shape B=%d L=%d n_all=%d Q=%d", fn, B, L, n_all, Q);
-  if (Q > 4)
-    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > 4 not supported by this build", fn, Q);
+  if (Q > kWideMaxQ)
+    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build", fn, Q,
+                     kWideMaxQ);
   sh->B = B;
   sh->L = L;
   sh->n_all = n_all;
@@ -1102,6 +1051,34 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
   if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  if (Q > 4) {
+    WideCall c;
+    c.phase = phase;
+    c.soft = tau > 0.0f;
+    c.steps = plan + TREX_PLAN_HEADER_INTS;
+    c.leaves = leaves;
+    c.cost = cost;
+    c.B = B;
+    c.L = L;
+    c.nl = s.nl;
+    c.ni = s.ni;
+    c.Q = Q;
+    c.n_slots = n_slots;
+    tau_coefs(tau, &c.a, &c.bcoef);
+    c.hard_root = (flags & TREX_FLAG_HARD_ROOT) ? 1 : 0;
+    c.dp = dp;
+    c.site_score = site_score;
+    c.tree_score = tree_score;
+    c.dts = dts;
+    c.marg = marg;
+    c.anc = anc;
+    c.d_cost = d_cost;
+    c.workspace = workspace;
+    c.stream = stream;
+    return wide_run(fn, c);
+  }
+  if ((int64_t)s.ni * L * Q * 4 > 0x7FFFFFF0LL)
+    return set_error(TREX_E_UNSUPPORTED, "%s: one tree's DP table exceeds 2 GiB", fn);
   const int spt = pick_spt(L, n_slots, s.nl, Q);
   const int tiles = tiles_for(L, spt);
   const size_t lds = lds_bytes(n_slots, s.nl, Q, spt);
@@ -1154,10 +1131,13 @@ using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 2; }
+extern "C" int trex_version(void) { return 3; }
+
+extern "C" int trex_dp_site_major(int Q) { return Q > 4 ? 1 : 0; }
 
 extern "C" int64_t trex_workspace_bytes(int B, int L, int n_all, int Q) {
   if (B <= 0 || L <= 0 || Q <= 0) return 0;
+  if (Q > 4) return wide_workspace_bytes(B, L, Q);
   const int64_t nb = (int64_t)B * tiles_for(L, 1);
   return counters_bytes(B) + nb * 8 * (1 + (int64_t)Q * Q) + (int64_t)Q * Q * B * 8 + 256;
 }
@@ -1214,11 +1194,12 @@ extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, con
                      "topology (cyclic child references)");
   if (!plan || !cost || !dp || !anc_states)
     return set_error(TREX_E_ARG, "trex_sankoff_backtrack: null pointer argument");
+  const int32_t* bt32 = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 4;
+  if (Q > 4) return wide_backtrack(bt32, cost, dp, B, L, s.ni, Q, anc_states, stream);
   const int spt = (L % 4 == 0) ? 4 : 1;
   const int tiles = tiles_for(L, spt);
   hipStream_t st = (hipStream_t)stream;
-  const int2* bt = reinterpret_cast<const int2*>(plan + TREX_PLAN_HEADER_INTS +
-                                                 (int64_t)B * s.ni * 4);
+  const int2* bt = reinterpret_cast<const int2*>(bt32);
 #define TREX_BT(QQ)                                                                            \
   if (spt == 4)                                                                                \
     hipLaunchKernelGGL((sankoff_backtrack_kernel<QQ, 4>), dim3(B * tiles), dim3(kWave), 0, st, \
@@ -1237,7 +1218,7 @@ extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, con
 
 extern "C" int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,
                                       int n_all, int Q, float* out, void* stream) {
-  if (B <= 0 || L <= 0 || n_all < 3 || Q < 2 || !dp || !leaves || !out)
+  if (B <= 0 || L <= 0 || n_all < 3 || Q < 2 || Q > kWideMaxQ || !dp || !leaves || !out)
     return set_error(TREX_E_ARG, "trex_dp_to_trex_layout: bad arguments");
   const int nl = (n_all + 1) / 2;
   const size_t total = (size_t)B * n_all * L;

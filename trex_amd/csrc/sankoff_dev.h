@@ -1,0 +1,80 @@
+// Device helpers shared by the Sankoff kernels (sankoff.hip: Q <= 4,
+// sites-per-lane; sankoff_wide.hip: Q > 4, states-per-lane).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace trex {
+namespace {
+
+constexpr float kSentinel = 1e5f;  // sankoff.py:152
+constexpr int kWave = 64;
+constexpr int kKindLeaf = 1, kKindInt = 2;  // 0 = 1e5 sentinel row
+
+// Read-only, wave-uniform data (topology program, cost matrix) goes through
+// the constant address space so hipcc emits scalar loads (s_load): vector
+// loads would be ordered behind the wave's in-flight DP-table stores in vmcnt.
+template <class T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <class T>
+__device__ __forceinline__ cptr<T> as_const(const T* p) {
+  return (cptr<T>)(p);
+}
+
+struct I4 {
+  int x, y, z, w;
+};
+__device__ __forceinline__ I4 load_step(cptr<int> prog, int k) {
+  return I4{prog[4 * k], prog[4 * k + 1], prog[4 * k + 2], prog[4 * k + 3]};
+}
+
+__device__ __forceinline__ float uniform(float x) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
+
+// SGPR cost-matrix modes: kHard (min-plus), kSoftK (factored softmin with
+// K = exp(-(C - cmin)/tau)), kSoftDirect (per-row stabilised softmin, used
+// when range(C)/tau > 40 would underflow K).
+constexpr int kHard = 0, kSoftK = 1, kSoftDirect = 2;
+
+// range(C)/tau <= 40: the factored form keeps every K >= e^-40
+__device__ __forceinline__ bool use_ktrick(float cmin, float cmax, float a) {
+  return (cmax - cmin) * a <= 57.70780f;  // log2(e^40)
+}
+
+// ---- buffer (SRD) access: 32-bit lane offset in voffset, row offset in
+// soffset, no 64-bit VALU address arithmetic per access ----
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ void store_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum of n values (lane-strided, fixed order) -> every lane
+__device__ __forceinline__ double wave_sum_strided(const double* p, int n, int lane) {
+  double v = 0.0;
+  for (int t = lane; t < n; t += kWave) v += load_sc1(p + t);
+  return wave_sum(v);
+}
+
+}  // namespace
+}  // namespace trex

@@ -1,0 +1,657 @@
+// libtrexhip.so -- Sankoff DP for Q > 4 states (protein: Q = 20), gfx950.
+//
+// Same semantics as sankoff.hip (trex src/trex/sankoff.py run_dp :24-94,
+// run_sankoff :114-188, backtrack :191-267, and the build-defined softmin
+// adjoint), different mapping.  With Q = 20 a lane-per-site kernel would hold
+// Q^2 = 400 dC accumulators per lane; here the STATE axis is spread over
+// lanes instead:
+//   * a group of G lanes (G = 8 / 16 / 20 / 32 >= Q) owns one site, lane i of
+//     the group owns parent state i; a 64-lane wave holds 64 / G sites;
+//   * lane i keeps row i and column i of C (or of K = exp(-(C - cmin)/tau))
+//     in VGPRs and accumulates row i of dC -- G accumulators per lane;
+//   * the all-to-all inside a site (every parent state needs every child
+//     state) goes through a 64-float LDS exchange buffer per wave: one
+//     ds_write_b32 + G/4 ds_read_b128 per exchanged vector;
+//   * the DP table is site-major, [B][n_int][L][Q]: a wave's row store is
+//     64/G * Q * 4 contiguous bytes.
+// Padded states (Q < G) are inert: their D is +inf on every exchange, their
+// cotangent 0, their C entries +inf / K entries 0.
+// Partial sums go to the workspace per wave and are reduced by a second,
+// fixed-order kernel (bitwise reproducible, no counters).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "sankoff_dev.h"
+#include "trex_common.h"
+
+namespace trex {
+
+namespace {
+
+struct WArgs {
+  const int* steps;  // [B][n_int] x int4 (plan.cpp)
+  const int8_t* leaves;
+  const float* cost;
+  int n_int, nl, L, tiles, B, n_slots, Q;
+  float a, bcoef;
+  int hard_root;
+  float* dp;          // [B][n_int][L][Q]
+  float* site_score;  // [B][L] or null
+  const float* dts;   // [B] or null
+  float* marg;        // [B][n_int][L][Q] or null
+  int8_t* anc;        // [B][n_int][L] or null
+  double* part_tree;  // [B * tiles]
+  double* part_dc;    // [Q * Q][B * tiles]
+};
+
+// LDS map (floats): 4 exchange buffers [4][64], leaf message table
+// T[Q + 1][G] (row Q = message of the all-1e5 row), IK[Q][G] = 1 / K[i][code],
+// slots [n_slots + 1][64] (n_slots = root cotangent), leaf tile [nl][64/G] i8
+constexpr int kXchg = 4 * kWave;
+
+__host__ __device__ constexpr int wide_tab_floats(int G, int Q) { return (2 * Q + 1) * G; }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// every lane publishes v; each lane gets the G values of its own group
+template <int G>
+__device__ __forceinline__ void xchg(float* x, int lane, int gbase, float v, float (&o)[G]) {
+  x[lane] = v;
+  wave_sync();
+#pragma unroll
+  for (int t = 0; t < G / 4; ++t) {
+    const float4 w = reinterpret_cast<const float4*>(x + gbase)[t];
+    o[4 * t] = w.x;
+    o[4 * t + 1] = w.y;
+    o[4 * t + 2] = w.z;
+    o[4 * t + 3] = w.w;
+  }
+  wave_sync();
+}
+
+__device__ __forceinline__ float wave_minf(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+// row[j] / col[j]: C[i][j] / C[j][i] (hard, direct) or K[i][j] / K[j][i] (K mode)
+template <int G>
+struct WCoef {
+  float row[G];
+  float col[G];
+  float cmin;
+};
+
+struct WLane {
+  int lane, i, gbase;
+  bool pad;  // state i >= Q
+};
+
+// message to parent state i:  min_j / smin_j (C[i][j] + D[j])   (sankoff.py:67-68)
+template <int G, int MODE>
+__device__ __forceinline__ float wmsg(const WCoef<G>& cf, float* X, const WLane& w, float a,
+                                      float bcoef, float D) {
+  float d[G];
+  xchg<G>(X, w.lane, w.gbase, w.pad ? INFINITY : D, d);
+  if constexpr (MODE == kHard) {
+    float v = cf.row[0] + d[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) v = fminf(v, cf.row[j] + d[j]);
+    return v;
+  } else if constexpr (MODE == kSoftK) {
+    float md = d[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) md = fminf(md, d[j]);
+    const float u = w.pad ? 0.0f : fast_exp2((md - D) * a);
+    float uu[G];
+    xchg<G>(X + kWave, w.lane, w.gbase, u, uu);
+    float s = cf.row[0] * uu[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) s = fmaf(cf.row[j], uu[j], s);
+    return fmaf(-bcoef, fast_log2(s), md + cf.cmin);
+  } else {
+    float x[G];
+    float mn = INFINITY;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      x[j] = cf.row[j] + d[j];
+      mn = fminf(mn, x[j]);
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < G; ++j) s += fast_exp2((mn - x[j]) * a);
+    return fmaf(-bcoef, fast_log2(s), mn);
+  }
+}
+
+// adjoint of one child message: acc[j] += g_i w_ij (row i of dC; in the K
+// form the K[i][j] factor is applied once at the end); returns the child's
+// cotangent for state i:  gc_i = sum_p g_p w_pi
+template <int G, int MODE>
+__device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane& w, float a,
+                                      float D, float g, float (&acc)[G]) {
+  float d[G];
+  xchg<G>(X, w.lane, w.gbase, w.pad ? INFINITY : D, d);
+  float rr[G];
+  if constexpr (MODE == kSoftK) {
+    float md = d[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) md = fminf(md, d[j]);
+    const float u = w.pad ? 0.0f : fast_exp2((md - D) * a);
+    float uu[G];
+    xchg<G>(X + kWave, w.lane, w.gbase, u, uu);
+    float s = cf.row[0] * uu[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) s = fmaf(cf.row[j], uu[j], s);
+    const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(s);
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc[j] = fmaf(r, uu[j], acc[j]);
+    xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
+    float t = rr[0] * cf.col[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) t = fmaf(rr[j], cf.col[j], t);
+    return u * t;
+  } else if constexpr (MODE == kHard) {
+    float x[G];
+    float mn = cf.row[0] + d[0];
+    x[0] = mn;
+#pragma unroll
+    for (int j = 1; j < G; ++j) {
+      x[j] = cf.row[j] + d[j];
+      mn = fminf(mn, x[j]);
+    }
+    float cnt = 0.0f;
+#pragma unroll
+    for (int j = 0; j < G; ++j) cnt += (x[j] == mn) ? 1.0f : 0.0f;
+    const float r = w.pad ? 0.0f : g / cnt;
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc[j] += (x[j] == mn) ? r : 0.0f;
+    float mm[G];
+    xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
+    xchg<G>(X + 3 * kWave, w.lane, w.gbase, w.pad ? 0.0f : mn, mm);
+    // parent p's x_{p i} = C[p][i] + D_i, bit-identical to lane p's x[i]
+    float gc = 0.0f;
+#pragma unroll
+    for (int p = 0; p < G; ++p) gc += (cf.col[p] + D == mm[p]) ? rr[p] : 0.0f;
+    return gc;
+  } else {
+    float x[G];
+    float mn = INFINITY;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      x[j] = cf.row[j] + d[j];
+      mn = fminf(mn, x[j]);
+    }
+    float e[G];
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      e[j] = fast_exp2((mn - x[j]) * a);
+      s += e[j];
+    }
+    const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(s);
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc[j] += r * e[j];
+    float mm[G];
+    xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
+    xchg<G>(X + 3 * kWave, w.lane, w.gbase, w.pad ? 0.0f : mn, mm);
+    float gc = 0.0f;
+#pragma unroll
+    for (int p = 0; p < G; ++p) gc += rr[p] * fast_exp2((mm[p] - (cf.col[p] + D)) * a);
+    return gc;
+  }
+}
+
+template <int G, int MODE, int PHASE, bool LFAST>
+__device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, float* lds) {
+  constexpr bool SOFT = MODE != kHard;
+  constexpr bool FWD = (PHASE & 1) != 0;
+  constexpr bool BWD = (PHASE & 2) != 0;
+  constexpr int SPW = kWave / G;
+  const int Q = A.Q;
+  const int tree = blockIdx.x / A.tiles;
+  const int tile = blockIdx.x - tree * A.tiles;
+  const int lane = threadIdx.x;
+  const int grp = lane / G;
+  WLane w;
+  w.lane = lane;
+  w.i = lane - grp * G;
+  w.gbase = (grp < SPW ? grp : 0) * G;
+  w.pad = w.i >= Q;
+  const int site = tile * SPW + grp;
+  const bool active = grp < SPW && site < A.L;
+  const int L = A.L;
+  const float a = A.a, bcoef = A.bcoef;
+
+  float* X = lds;
+  float* tab = lds + kXchg;                       // T[code][i]
+  float* itab = tab + (Q + 1) * G;                // IK[code][i]
+  float* slots = lds + kXchg + wide_tab_floats(G, Q);
+  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (A.n_slots + 1) * kWave);
+
+  // ---- prologue: leaf tables + leaf tile ----
+  {
+    const float sent = wmsg<G, MODE>(cf, X, w, a, bcoef, kSentinel);
+    if (grp == 0) {
+      for (int code = 0; code < Q; ++code) {
+        const float cv = w.pad ? INFINITY : A.cost[w.i * Q + code];
+        tab[code * G + w.i] = cv;
+        if constexpr (MODE == kSoftK) itab[code * G + w.i] = w.pad ? 0.0f : fast_exp2((cv - cf.cmin) * a);
+      }
+      tab[Q * G + w.i] = sent;
+    }
+    const int8_t* lv = A.leaves + (size_t)tree * A.nl * L;
+    for (int t = lane; t < A.nl * SPW; t += kWave) {
+      const int leaf = t / SPW;
+      const int s = tile * SPW + (t - leaf * SPW);
+      int code = s < L ? (int)lv[(size_t)leaf * L + s] : Q;
+      code = ((unsigned)code < (unsigned)Q) ? code : Q;
+      lleaf[t] = (int8_t)code;
+    }
+    wave_sync();
+  }
+
+  const cptr<int> prog = as_const(A.steps) + (size_t)tree * A.n_int * 4;
+  const uint32_t rowbytes = (uint32_t)L * Q * 4;
+  const uint32_t treebytes = (uint32_t)A.n_int * rowbytes;
+  const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * A.n_int * L * Q, treebytes);
+  // inactive sites and padded states address past the buffer: stores drop, loads give 0
+  const int voff = (active && !w.pad) ? (site * Q + w.i) * 4 : 0x7FFFFFF0;
+  const int lgrp = grp < SPW ? grp : 0;
+
+  float dv = 0.0f;
+  if constexpr (FWD) {
+    I4 nxt = load_step(prog, 0);
+    for (int k = 0; k < A.n_int; ++k) {
+      const I4 stp = nxt;
+      if (k + 1 < A.n_int) nxt = load_step(prog, k + 1);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? stp.y : stp.z;
+        const int kind = (desc >> 24) & 3;
+        float m;
+        if (kind == kKindLeaf) {
+          const int code = lleaf[(desc & 0xFFFF) * SPW + lgrp];
+          if constexpr (LFAST) {
+            m = tab[code * G + w.i];
+          } else {
+            m = wmsg<G, MODE>(cf, X, w, a, bcoef, code == w.i ? 0.0f : kSentinel);
+          }
+        } else if (kind == kKindInt) {
+          m = wmsg<G, MODE>(cf, X, w, a, bcoef, slots[((desc >> 16) & 0xFF) * kWave + lane]);
+        } else {
+          m = tab[Q * G + w.i];
+        }
+        dv = (c == 0) ? m : dv + m;
+      }
+      const int row = stp.x & 0xFFFF;
+      const int oslot = (stp.x >> 16) & 0xFF;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rdp, voff, row * rowbytes, 0);
+      if (oslot != 0xFF) slots[oslot * kWave + lane] = dv;
+    }
+  } else {
+    dv = __uint_as_float(
+        __builtin_amdgcn_raw_buffer_load_b32(rdp, voff, (A.n_int - 1) * rowbytes, 0));
+  }
+
+  // ---- root: score + cotangent (sankoff.py:187) ----
+  float groot, score;
+  {
+    float d[G];
+    xchg<G>(X, lane, w.gbase, w.pad ? INFINITY : dv, d);
+    float mn = d[0];
+#pragma unroll
+    for (int j = 1; j < G; ++j) mn = fminf(mn, d[j]);
+    if (!SOFT || A.hard_root) {
+      float cnt = 0.0f;
+#pragma unroll
+      for (int j = 0; j < G; ++j) cnt += (d[j] == mn) ? 1.0f : 0.0f;
+      groot = (!w.pad && dv == mn) ? 1.0f / cnt : 0.0f;
+      score = mn;
+    } else {
+      const float e = w.pad ? 0.0f : fast_exp2((mn - dv) * a);
+      float ee[G];
+      xchg<G>(X + kWave, lane, w.gbase, e, ee);
+      float s = 0.0f;
+#pragma unroll
+      for (int j = 0; j < G; ++j) s += ee[j];
+      groot = e * __builtin_amdgcn_rcpf(s);
+      score = fmaf(-bcoef, fast_log2(s), mn);
+    }
+  }
+  const bool leader = active && w.i == 0;
+  if constexpr (FWD) {
+    if (leader && A.site_score) A.site_score[(size_t)tree * L + site] = score;
+    const double tot = wave_sum(leader ? (double)score : 0.0);
+    if (lane == 0) A.part_tree[blockIdx.x] = tot;
+  }
+
+  if constexpr (BWD) {
+    float acc[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc[j] = 0.0f;
+    const float dscale = A.dts ? as_const(A.dts)[tree] : 1.0f;
+    slots[A.n_slots * kWave + lane] = active ? groot * dscale : 0.0f;
+    const bool want_marg = A.marg != nullptr;
+    const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * A.n_int * L * Q : A.dp,
+                                 treebytes);
+    const bool want_anc = A.anc != nullptr;
+    int8_t* at = want_anc ? A.anc + (size_t)tree * A.n_int * L + site : nullptr;
+
+    // the next step's internal-child DP values are loaded one step ahead
+    float nd[2] = {0.0f, 0.0f};
+    I4 nstp = load_step(prog, A.n_int - 1);
+    auto prefetch = [&](const I4& s2) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? s2.y : s2.z;
+        if (((desc >> 24) & 3) == kKindInt)
+          nd[c] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rdp, voff, (desc & 0xFFFF) * rowbytes, 0));
+      }
+    };
+    prefetch(nstp);
+    for (int k = A.n_int - 1; k >= 0; --k) {
+      const I4 stp = nstp;
+      const float cd0 = nd[0], cd1 = nd[1];
+      if (k > 0) {
+        nstp = load_step(prog, k - 1);
+        prefetch(nstp);
+      }
+      if (stp.w & kStepUnreached) continue;
+      const int row = stp.x & 0xFFFF;
+      const float g = slots[((stp.w & kStepRoot) ? A.n_slots : ((stp.x >> 16) & 0xFF)) * kWave + lane];
+      if (want_marg)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), rmg, voff, row * rowbytes, 0);
+      if (want_anc) {
+        float gg[G];
+        xchg<G>(X, lane, w.gbase, w.pad ? -INFINITY : g, gg);
+        float bv = gg[0];
+        int bi = 0;
+#pragma unroll
+        for (int j = 1; j < G; ++j)
+          if (gg[j] > bv) { bv = gg[j]; bi = j; }
+        if (leader) at[(size_t)row * L] = (int8_t)bi;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int desc = c == 0 ? stp.y : stp.z;
+        const int kind = (desc >> 24) & 3;
+        if (kind == kKindLeaf) {
+          const int code = lleaf[(desc & 0xFFFF) * SPW + lgrp];
+          bool onehot = false;
+          if constexpr (LFAST) onehot = !__any(active && code == Q);
+          if (onehot) {
+            // exact leaf weights are one-hot: dC[i][code] += g_i (/ K[i][code])
+            float t = g;
+            if constexpr (MODE == kSoftK) t = g * itab[code * G + w.i];
+            if (w.pad) t = 0.0f;
+#pragma unroll
+            for (int j = 0; j < G; ++j) acc[j] += (code == j) ? t : 0.0f;
+          } else {
+            (void)wadj<G, MODE>(cf, X, w, a, code == w.i ? 0.0f : kSentinel, g, acc);
+          }
+        } else if (kind == kKindInt) {
+          float gc = wadj<G, MODE>(cf, X, w, a, c == 0 ? cd0 : cd1, g, acc);
+          const int cslot = (desc >> 16) & 0xFF;
+          if (desc & kStepAccumulate) gc += slots[cslot * kWave + lane];
+          slots[cslot * kWave + lane] = gc;
+        } else {
+          (void)wadj<G, MODE>(cf, X, w, a, kSentinel, g, acc);
+        }
+      }
+    }
+
+    // ---- per-wave dC partial: rows i summed over the wave's sites ----
+    const int nb = A.B * A.tiles;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      double v = (double)acc[j];
+      if constexpr (MODE == kSoftK) v *= (double)cf.row[j];
+      double s = v;  // group 0 sums the groups in order
+#pragma unroll
+      for (int gq = 1; gq < SPW; ++gq) s += __shfl(v, w.i + gq * G, kWave);
+      if (grp == 0 && !w.pad && j < Q) A.part_dc[(size_t)(w.i * Q + j) * nb + blockIdx.x] = s;
+    }
+  }
+}
+
+template <int G, int MODE, int PHASE>
+__device__ __forceinline__ void wide_dispatch_leaf(const WArgs& A, const WCoef<G>& cf, float cmax,
+                                                   float* lds) {
+  const float range = cmax - cf.cmin;
+  const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
+  if (lfast)
+    wide_body<G, MODE, PHASE, true>(A, cf, lds);
+  else
+    wide_body<G, MODE, PHASE, false>(A, cf, lds);
+}
+
+template <int G, bool SOFT, int PHASE>
+__global__ __launch_bounds__(kWave) void sankoff_wide_kernel(WArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int Q = A.Q;
+  const int i = threadIdx.x % G;
+  const bool pad = i >= Q;
+  WCoef<G> cf;
+  float lmin = INFINITY, lmax = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const bool ok = !pad && j < Q;
+    cf.row[j] = ok ? A.cost[i * Q + j] : INFINITY;
+    cf.col[j] = ok ? A.cost[j * Q + i] : INFINITY;
+    if (ok) {
+      lmin = fminf(lmin, cf.row[j]);
+      lmax = fmaxf(lmax, cf.row[j]);
+    }
+  }
+  cf.cmin = uniform(wave_minf(lmin));
+  const float cmax = uniform(wave_maxf(lmax));
+  if constexpr (!SOFT) {
+    wide_dispatch_leaf<G, kHard, PHASE>(A, cf, cmax, lds);
+  } else if (use_ktrick(cf.cmin, cmax, A.a)) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      cf.row[j] = (!pad && j < Q) ? fast_exp2((cf.cmin - cf.row[j]) * A.a) : 0.0f;
+      cf.col[j] = (!pad && j < Q) ? fast_exp2((cf.cmin - cf.col[j]) * A.a) : 0.0f;
+    }
+    wide_dispatch_leaf<G, kSoftK, PHASE>(A, cf, cmax, lds);
+  } else {
+    wide_dispatch_leaf<G, kSoftDirect, PHASE>(A, cf, cmax, lds);
+  }
+}
+
+// fixed-order reduction of the per-wave partials: blocks [0, B) = tree
+// scores, blocks [B, B + Q*Q) = dC entries
+__global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restrict__ part_tree,
+                                                          const double* __restrict__ part_dc,
+                                                          int B, int tiles, int Q2, int do_tree,
+                                                          float* __restrict__ tree_score,
+                                                          float* __restrict__ d_cost) {
+  __shared__ double red[256];
+  const int b = blockIdx.x;
+  const double* src;
+  int n;
+  float* dst;
+  if (do_tree && b < B) {
+    src = part_tree + (size_t)b * tiles;
+    n = tiles;
+    dst = tree_score + b;
+  } else {
+    const int q = b - (do_tree ? B : 0);
+    const size_t nb = (size_t)B * tiles;
+    src = part_dc + (size_t)q * nb;
+    n = (int)nb;
+    dst = d_cost + q;
+  }
+  double v = 0.0;
+  for (int t = threadIdx.x; t < n; t += 256) v += src[t];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *dst = (float)red[0];
+}
+
+// trex-exact ancestral reconstruction on the site-major table
+// (sankoff.py:166-185, 191-267): one lane per site, C in LDS
+__global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __restrict__ bt,
+                                                               const float* __restrict__ cost,
+                                                               const float* __restrict__ dp,
+                                                               int n_int, int L, int Q, int tiles,
+                                                               int8_t* __restrict__ anc) {
+  __shared__ float c[32 * 32];
+  const int tree = blockIdx.x / tiles;
+  const int tile = blockIdx.x - tree * tiles;
+  const int lane = threadIdx.x;
+  for (int t = lane; t < Q * Q; t += kWave) c[t] = cost[t];
+  __syncthreads();
+  const int site = tile * kWave + lane;
+  if (site >= L) return;
+  const cptr<int> prog = as_const(bt) + (size_t)tree * n_int * 2;
+  const float* dpt = dp + (size_t)tree * n_int * L * Q + (size_t)site * Q;
+  int8_t* at = anc + (size_t)tree * n_int * L + site;
+  for (int k = 0; k < n_int; ++k) {
+    const int ex = prog[2 * k], ey = prog[2 * k + 1];
+    const int x = ex & 0xFFFF;
+    const int kind = (ex >> 16) & 0xF;
+    int out = 0;
+    if (kind != kBtUnreached) {
+      const float* d = dpt + (size_t)x * L * Q;
+      const bool sent = kind == kBtSentinel;
+      if (kind == kBtRoot) {
+        float bv = d[0];
+        for (int j = 1; j < Q; ++j) {
+          const float v = d[j];
+          if (v < bv) { bv = v; out = j; }
+        }
+      } else {
+        const int sp = at[(size_t)ey * L];
+        const float* row = c + sp * Q;
+        float bv = row[0] + (sent ? kSentinel : d[0]);
+        for (int j = 1; j < Q; ++j) {
+          const float v = row[j] + (sent ? kSentinel : d[j]);
+          if (v < bv) { bv = v; out = j; }
+        }
+      }
+    }
+    at[(size_t)x * L] = (int8_t)out;
+  }
+}
+
+template <int G, bool SOFT>
+void launch_wide(int phase, int grid, size_t lds, hipStream_t st, const WArgs& A) {
+  if (phase == 1)
+    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 1>), dim3(grid), dim3(kWave), lds, st, A);
+  else if (phase == 2)
+    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 2>), dim3(grid), dim3(kWave), lds, st, A);
+  else
+    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 3>), dim3(grid), dim3(kWave), lds, st, A);
+}
+
+template <int G>
+void launch_wide_g(int phase, bool soft, int grid, size_t lds, hipStream_t st, const WArgs& A) {
+  if (soft)
+    launch_wide<G, true>(phase, grid, lds, st, A);
+  else
+    launch_wide<G, false>(phase, grid, lds, st, A);
+}
+
+}  // namespace
+
+int wide_group(int Q) {
+  if (Q <= 8) return 8;
+  if (Q <= 16) return 16;
+  if (Q <= 20) return 20;
+  return 32;
+}
+
+int wide_tiles(int L, int Q) {
+  const int spw = kWave / wide_group(Q);
+  return (L + spw - 1) / spw;
+}
+
+size_t wide_lds_bytes(int n_slots, int nl, int Q) {
+  const int G = wide_group(Q);
+  const size_t b = (size_t)(kXchg + wide_tab_floats(G, Q) + (n_slots + 1) * kWave) * 4 +
+                   (size_t)nl * (kWave / G);
+  return (b + 15) & ~(size_t)15;
+}
+
+int64_t wide_workspace_bytes(int B, int L, int Q) {
+  const int64_t nb = (int64_t)B * wide_tiles(L, Q);
+  return nb * 8 * (1 + (int64_t)Q * Q) + 256;
+}
+
+int wide_run(const char* fn, const WideCall& c) {
+  const int tiles = wide_tiles(c.L, c.Q);
+  const size_t lds = wide_lds_bytes(c.n_slots, c.nl, c.Q);
+  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
+  if ((int64_t)c.B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
+  if ((int64_t)c.ni * c.L * c.Q * 4 > 0x7FFFFFF0LL)
+    return set_error(TREX_E_UNSUPPORTED, "%s: one tree's DP table exceeds 2 GiB", fn);
+  WArgs A;
+  A.steps = c.steps;
+  A.leaves = c.leaves;
+  A.cost = c.cost;
+  A.n_int = c.ni;
+  A.nl = c.nl;
+  A.L = c.L;
+  A.tiles = tiles;
+  A.B = c.B;
+  A.n_slots = c.n_slots;
+  A.Q = c.Q;
+  A.a = c.a;
+  A.bcoef = c.bcoef;
+  A.hard_root = c.hard_root;
+  A.dp = c.dp;
+  A.site_score = c.site_score;
+  A.dts = c.dts;
+  A.marg = c.marg;
+  A.anc = c.anc;
+  const int64_t nb = (int64_t)c.B * tiles;
+  A.part_tree = static_cast<double*>(c.workspace);
+  A.part_dc = A.part_tree + nb;
+  hipStream_t st = (hipStream_t)c.stream;
+  const int grid = (int)nb;
+  switch (wide_group(c.Q)) {
+    case 8: launch_wide_g<8>(c.phase, c.soft, grid, lds, st, A); break;
+    case 16: launch_wide_g<16>(c.phase, c.soft, grid, lds, st, A); break;
+    case 20: launch_wide_g<20>(c.phase, c.soft, grid, lds, st, A); break;
+    default: launch_wide_g<32>(c.phase, c.soft, grid, lds, st, A); break;
+  }
+  const bool do_tree = (c.phase & 1) != 0;
+  const bool do_dc = (c.phase & 2) != 0;
+  const int rgrid = (do_tree ? c.B : 0) + (do_dc ? c.Q * c.Q : 0);
+  hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(256), 0, st, A.part_tree, A.part_dc,
+                     c.B, tiles, c.Q * c.Q, do_tree ? 1 : 0, c.tree_score, c.d_cost);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return TREX_OK;
+}
+
+int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
+                   int Q, int8_t* anc, void* stream) {
+  const int tiles = (L + kWave - 1) / kWave;
+  hipLaunchKernelGGL(wide_backtrack_kernel, dim3(B * tiles), dim3(kWave), 0, (hipStream_t)stream,
+                     bt, cost, dp, ni, L, Q, tiles, anc);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return set_error(TREX_E_HIP, "trex_sankoff_backtrack: %s", hipGetErrorString(e));
+  return TREX_OK;
+}
+
+}  // namespace trex

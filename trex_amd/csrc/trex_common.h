@@ -2,6 +2,7 @@
 #pragma once
 
 #include <cstdarg>
+#include <cstddef>
 #include <cstdint>
 #include <cstdio>
 
@@ -24,5 +25,34 @@ constexpr int kBtSentinel = 2;
 constexpr int kBtUnreached = 3;
 
 int set_error(int code, const char* fmt, ...);
+
+// ---- Q > 4: state-parallel kernels on a site-major DP table (sankoff_wide.hip)
+struct WideCall {
+  int phase;  // 1 fwd, 2 adjoint, 3 fused
+  bool soft;
+  const int* steps;
+  const int8_t* leaves;
+  const float* cost;
+  int B, L, nl, ni, Q, n_slots;
+  float a, bcoef;
+  int hard_root;
+  float* dp;
+  float* site_score;
+  float* tree_score;
+  const float* dts;
+  float* marg;
+  int8_t* anc;
+  float* d_cost;
+  void* workspace;
+  void* stream;
+};
+constexpr int kWideMaxQ = 32;
+int wide_group(int Q);
+int wide_tiles(int L, int Q);
+size_t wide_lds_bytes(int n_slots, int nl, int Q);
+int64_t wide_workspace_bytes(int B, int L, int Q);
+int wide_run(const char* fn, const WideCall& c);
+int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
+                   int Q, int8_t* anc, void* stream);
 
 }  // namespace trex

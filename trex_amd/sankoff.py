@@ -55,7 +55,7 @@ def leaf_codes(sequences, n_states: int, device=None):
 @dataclass
 class ForwardResult:
     tree_score: "object"  # (B,) float32
-    dp: "object"  # (B, n_int, Q, L) float32 or None
+    dp: "object"  # (B, n_int, Q, L) float32 ((B, n_int, L, Q) for Q > 4)
     site_score: "object"  # (B, L) float32 or None
 
 
@@ -82,7 +82,14 @@ class SankoffEngine:
 
     # -- shapes ------------------------------------------------------------
     @property
+    def site_major(self) -> bool:
+        """Q > 4 tables are site-major (lane-per-state kernels, trex_hip.h)."""
+        return bool(lib().trex_dp_site_major(self.Q))
+
+    @property
     def dp_shape(self):
+        if self.site_major:
+            return (self.plan.B, self.plan.n_int, self.L, self.Q)
         return (self.plan.B, self.plan.n_int, self.Q, self.L)
 
     def _check_inputs(self, leaves, cost):
@@ -215,7 +222,7 @@ class SankoffEngine:
         return f.tree_score, dc
 
     def to_trex_layout(self, dp, leaves):
-        """(B, n_int, Q, L) -> trex VmappedDPTable per tree: (B, L, n_all, Q)."""
+        """engine dp table -> trex VmappedDPTable per tree: (B, L, n_all, Q)."""
         torch = _torch()
         p = self.plan
         out = torch.empty((p.B, self.L, p.n_all, self.Q), dtype=torch.float32,
