@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly, no hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 single-tree line")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 protein line")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 tree-cost loop line")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -152,6 +153,93 @@ def c2_line(torch, device, args, cpu_threads):
     out["cpu_port_ms"] = cpu_s * 1e3
     out["speedup_vs_cpu_port"] = cpu_s / gpu_s
     return out
+
+
+def _replay_seconds(torch, fn, n):
+    """Capture fn in a hipGraph, return mean wall seconds per replay."""
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    for _ in range(5):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n
+
+
+def c3_line(torch, device, cpu_threads):
+    """C3 (BASELINE.json configs[2]): balanced 64-taxa tree x 10 000 sites x
+    20 states (protein), C symmetric integer {1..4} off-diagonal (seed 3).
+    Two steps: (a) softmin tau=0.5 fwd + grad + marginals + soft ancestral
+    states in one fused launch; (b) trex-exact ancestral reconstruction
+    (hard forward + backtrack, run_sankoff(return_path=True))."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _cases import int_cost, simulate_leaves
+
+    from trex_amd import SankoffEngine, TreePlan, children_from_adjacency
+
+    nl, L, Q, tau = 64, 10000, 20, 0.5
+    n_int = nl - 1
+    seqs, adj = simulate_leaves(nl, L, Q, 50, seed=2)
+    ch = children_from_adjacency(adj)
+    eng = SankoffEngine(TreePlan(ch), L, Q, device)
+    leaves = torch.from_numpy(np.ascontiguousarray(seqs[None, :nl])).to(device)
+    cost_np = int_cost(Q, seed=3)
+    cost = torch.from_numpy(cost_np).to(device)
+    f = torch.empty(eng.dp_shape, dtype=torch.float32, device=device)
+    out = {"dp": f, "tree_score": torch.empty(1, device=device),
+           "d_cost": torch.empty((Q, Q), device=device),
+           "marginals": torch.empty_like(f),
+           "anc_states": torch.empty((1, n_int, L), dtype=torch.int8, device=device)}
+
+    def soft():
+        eng.fwd_bwd(leaves, cost, tau, marginals=True, anc_states=True, out=out)
+
+    def hard():
+        r = eng.forward(leaves, cost, 0.0, out=out)
+        eng.backtrack(cost, r.dp)
+
+    soft_s = _replay_seconds(torch, soft, 200)
+    hard_s = _replay_seconds(torch, hard, 200)
+    # device time of the fused kernel alone (HIP events on torch's stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(20)]
+    for e0, e1 in ev:
+        e0.record()
+        soft()
+        e1.record()
+    torch.cuda.synchronize()
+    k_s = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e-3
+    units = L * n_int * Q
+    # algorithmic bytes: leaves in, dp + marginals out (f32), anc states out (i8)
+    abytes = L * (nl + 8 * Q * n_int + n_int)
+    res = {"workload": "C3: balanced 64-taxa tree x 10000 sites x 20 states, softmin tau=0.5 "
+                       "fwd+grad+marginals+soft ancestral (fused) | hard fwd + trex backtrack",
+           "soft_ms_per_step": soft_s * 1e3, "soft_value": units / soft_s,
+           "hard_recon_ms_per_step": hard_s * 1e3, "hard_recon_value": units / hard_s,
+           "unit": "site-node-state updates/s",
+           "roofline": {"bound": "hbm", "kernel": "sankoff_wide_kernel<20,soft,fused>+reduce",
+                        "achieved": round(abytes / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(abytes / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                        "algorithmic_bytes": abytes, "launch_us": round(k_s * 1e6, 2)}}
+    from oracle.cpu_port import fwd_bwd
+
+    fwd_bwd(ch, seqs[None, :nl], cost_np, tau, threads=cpu_threads)
+    reps = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        fwd_bwd(ch, seqs[None, :nl], cost_np, tau, threads=cpu_threads)
+        reps.append(time.perf_counter() - t0)
+    cpu_s = float(np.median(reps))
+    res["cpu_port_ms"] = cpu_s * 1e3
+    res["speedup_vs_cpu_port"] = cpu_s / soft_s
+    return res
 
 
 def c5_line(torch, device, steps=20, warmup=3):
@@ -350,6 +438,8 @@ def main():
                                                   tau, L, n, Q, threads)
         if not args.no_c2:
             result["c2"] = c2_line(torch, device, args, threads)
+        if not args.no_c3:
+            result["c3"] = c3_line(torch, device, threads)
         if not args.no_c5:
             result["c5"] = c5_line(torch, device)
     if rank == 0:

@@ -242,6 +242,41 @@ __device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT
   }
 }
 
+// packed FP32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes of work per VALU op)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk(float x, float y) { return f2{x, y}; }
+__device__ __forceinline__ void pfma(float& d0, float& d1, f2 a, f2 b) {
+  const f2 r = __builtin_elementwise_fma(a, b, f2{d0, d1});
+  d0 = r.x;
+  d1 = r.y;
+}
+// s_i = sum_j K[i][j] u[j] with row pairs of K (adjacent SGPRs)
+template <int Q>
+__device__ __forceinline__ float kdot(const float (&krow)[Q], const float (&u)[Q]) {
+  if constexpr (Q % 2 == 0) {
+    f2 acc = pk(krow[0], krow[1]) * pk(u[0], u[1]);
+#pragma unroll
+    for (int j = 2; j < Q; j += 2) acc = __builtin_elementwise_fma(pk(krow[j], krow[j + 1]), pk(u[j], u[j + 1]), acc);
+    return acc.x + acc.y;
+  } else {
+    float acc = krow[0] * u[0];
+#pragma unroll
+    for (int j = 1; j < Q; ++j) acc = fmaf(krow[j], u[j], acc);
+    return acc;
+  }
+}
+// acc[j] += r * v[j]
+template <int Q>
+__device__ __forceinline__ void axpy(float (&acc)[Q], float r, const float (&v)[Q]) {
+  if constexpr (Q % 2 == 0) {
+#pragma unroll
+    for (int j = 0; j < Q; j += 2) pfma(acc[j], acc[j + 1], pk(r, r), pk(v[j], v[j + 1]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < Q; ++j) acc[j] = fmaf(r, v[j], acc[j]);
+  }
+}
+
 // --------------------------------------------------------------------------
 // message M_c[i] = min_j / smin_j (C[i][j] + D_c[j])      (sankoff.py:67-68)
 // --------------------------------------------------------------------------
@@ -264,17 +299,13 @@ __device__ __forceinline__ void message(const Coef<Q>& cf, float a, float bcoef,
       float md = d[0][s];
 #pragma unroll
       for (int j = 1; j < Q; ++j) md = fminf(md, d[j][s]);
+      const float mda = md * a;
       float u[Q];
 #pragma unroll
-      for (int j = 0; j < Q; ++j) u[j] = fast_exp2((md - d[j][s]) * a);
+      for (int j = 0; j < Q; ++j) u[j] = fast_exp2(fmaf(-d[j][s], a, mda));
       const float base = md + cf.cmin;
 #pragma unroll
-      for (int i = 0; i < Q; ++i) {
-        float acc = cf.k[i][0] * u[0];
-#pragma unroll
-        for (int j = 1; j < Q; ++j) acc = fmaf(cf.k[i][j], u[j], acc);
-        m[i][s] = fmaf(-bcoef, fast_log2(acc), base);
-      }
+      for (int i = 0; i < Q; ++i) m[i][s] = fmaf(-bcoef, fast_log2(kdot<Q>(cf.k[i], u)), base);
     }
   } else {
 #pragma unroll
@@ -337,28 +368,23 @@ __device__ __forceinline__ void message_adjoint(const Coef<Q>& cf, float a,
       float md = d[0][s];
 #pragma unroll
       for (int j = 1; j < Q; ++j) md = fminf(md, d[j][s]);
+      const float mda = md * a;
       float u[Q];
 #pragma unroll
-      for (int j = 0; j < Q; ++j) u[j] = fast_exp2((md - d[j][s]) * a);
+      for (int j = 0; j < Q; ++j) u[j] = fast_exp2(fmaf(-d[j][s], a, mda));
       float r[Q];
 #pragma unroll
-      for (int i = 0; i < Q; ++i) {
-        float sm = cf.k[i][0] * u[0];
+      for (int i = 0; i < Q; ++i) r[i] = g[i][s] * __builtin_amdgcn_rcpf(kdot<Q>(cf.k[i], u));
 #pragma unroll
-        for (int j = 1; j < Q; ++j) sm = fmaf(cf.k[i][j], u[j], sm);
-        r[i] = g[i][s] * __builtin_amdgcn_rcpf(sm);
-      }
+      for (int i = 0; i < Q; ++i) axpy<Q>(acc[i], r[i], u);
+      // t[j] = sum_i r_i K[i][j] (row pairs of K), gc = u * t
+      float t[Q];
 #pragma unroll
-      for (int i = 0; i < Q; ++i)
+      for (int j = 0; j < Q; ++j) t[j] = r[0] * cf.k[0][j];
 #pragma unroll
-        for (int j = 0; j < Q; ++j) acc[i][j] = fmaf(r[i], u[j], acc[i][j]);
+      for (int i = 1; i < Q; ++i) axpy<Q>(t, r[i], cf.k[i]);
 #pragma unroll
-      for (int j = 0; j < Q; ++j) {
-        float t = r[0] * cf.k[0][j];
-#pragma unroll
-        for (int i = 1; i < Q; ++i) t = fmaf(r[i], cf.k[i][j], t);
-        gc[j][s] = u[j] * t;
-      }
+      for (int j = 0; j < Q; ++j) gc[j][s] = u[j] * t[j];
     } else {
 #pragma unroll
       for (int j = 0; j < Q; ++j) gc[j][s] = 0.0f;
@@ -448,358 +474,376 @@ struct KArgs {
   float* marg;          // [B][n_int][Q][L] or null
   int8_t* anc;          // [B][n_int][L] or null
   float* d_cost;        // [Q][Q]
-  double* part_tree;    // [B*tiles]
-  double* part_dc;      // [Q*Q][B*tiles]
-  double* tree_dc;      // [Q*Q][B]
-  int* counters;        // [B+1], zero at rest (self-resetting)
+  double* part_tree;    // [B*tiles] per-item score partials
+  double* part_dc;      // [Q*Q][B*tiles] per-item dC partials
+  int nblocks;          // B * tiles work items
 };
 
 
 // LDS map (floats): [0, 64) leaf tables: T[code][i] (message; code Q =
-// missing leaf) at 0, IK[code][i] = 1/K[i][code] (factored-form leaf adjoint
-// weight) at 32; then slots [n_slots + 2][64][Q*SPT] (n_slots = root cotangent,
-// n_slots + 1 = all-1e5 sentinel row), then the leaf tile [nl][64][SPT] i8.
+// missing leaf / all-1e5 sentinel row) at 0, IK[code][i] = 1/K[i][code]
+// (factored-form leaf adjoint weight) at 32; then the slot stack
+// [n_slots + 1][64][Q*SPT] (slot n_slots = root cotangent), then the leaf
+// tile [nl][64*SPT] i8 (raw codes, normalised to [0, Q] at use).  The
+// all-1e5 sentinel rows live in registers.
 constexpr int kTabFloats = 64;
+constexpr int kPrefetchRows = 64;  // leaf tiles of <= 64 leaves are prefetched
 
+// Persistent waves: the grid holds as many waves as are co-resident; block
+// (x = blockIdx % 8, j = blockIdx / 8) walks the items of XCD x's contiguous
+// range with stride gridDim/8, so the waves of one XCD always work on
+// adjacent tiles (shared L2 lines).  Each item is one (tree, 64*SPT-site
+// tile); the next item's leaf tile is loaded into registers while the
+// current one computes.
 template <int Q, int SPT, int MODE, int PHASE, bool LFAST>
 __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
-  const int tree = blockIdx.x / A.tiles;
-  const int tile = blockIdx.x - tree * A.tiles;
   const int lane = threadIdx.x;
-  const int site = (tile * kWave + lane) * SPT;
-  const bool active = site < A.L;
-  const int sc = active ? site : 0;
   const int L = A.L;
   const float a = A.a, bcoef = A.bcoef;
+  const int nb = A.nblocks;
+  const int per = (nb + 7) / 8;
+  const int xcd = blockIdx.x & 7;
+  const int stride = gridDim.x >> 3;
+  const int item_end = min(nb, (xcd + 1) * per);
+  int item = xcd * per + (blockIdx.x >> 3);
+  if (item >= item_end) return;
 
   Coef<Q> cf;
   load_coef<Q, MODE>(A.cost, a, cf);
 
   float* tab = lds;
   float* slots = lds + kTabFloats;
-  const int kRootSlot = A.n_slots, kSentSlot = A.n_slots + 1;
-  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 2) * Q * kWave * SPT);
+  const int kRootSlot = A.n_slots;
+  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT);
 
-  // ---- prologue ----
-  {
-    // leaf message table: T[s][i] = C[i][s]; T[Q][i] = message of an all-1e5 row
-    if (lane < Q) {
-      float d1[Q][1], m1[Q][1];
+  // ---- once per wave: leaf message table T[s][i] = C[i][s], T[Q][i] =
+  // message of an all-1e5 row ----
+  if (lane < Q) {
+    float d1[Q][1], m1[Q][1];
 #pragma unroll
-      for (int j = 0; j < Q; ++j) d1[j][0] = kSentinel;
-      message<Q, 1, MODE>(cf, a, bcoef, d1, m1);
-#pragma unroll
-      for (int i = 0; i < Q; ++i)
-        if (i == lane) tab[Q * Q + i] = m1[i][0];
-#pragma unroll
-      for (int st_ = 0; st_ < Q; ++st_) {
-        const float cv = as_const(A.cost)[lane * Q + st_];
-        tab[st_ * Q + lane] = cv;
-        if constexpr (MODE == kSoftK) tab[32 + st_ * Q + lane] = fast_exp2((cv - cf.cmin) * a);
-      }
-    }
-    float sent[Q][SPT];
-    fill_sentinel<Q, SPT>(sent);
-    lds_put<Q, SPT>(slots, kSentSlot, lane, sent);
-    // leaf tile: codes normalised to [0, Q] (Q = trex's dropped scatter)
-    const int8_t* lv = A.leaves + (size_t)tree * A.nl * L + sc;
-    constexpr int kBatch = 16;
-    for (int c0 = 0; c0 < A.nl; c0 += kBatch) {
-      int code[kBatch][SPT];
-#pragma unroll
-      for (int u = 0; u < kBatch; ++u)
-        if (c0 + u < A.nl) ld_codes<SPT>(lv + (size_t)(c0 + u) * L, code[u]);
-#pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        if (c0 + u < A.nl) {
-#pragma unroll
-          for (int s = 0; s < SPT; ++s) code[u][s] = ((unsigned)code[u][s] < (unsigned)Q) ? code[u][s] : Q;
-          st_codes<SPT>(lleaf + ((c0 + u) * kWave + lane) * SPT, code[u]);
-        }
-      }
-    }
-    __syncthreads();  // the table is written by lanes < Q, read by all
-  }
-
-  const cptr<int> prog = as_const(reinterpret_cast<const int*>(A.steps)) + (size_t)tree * A.n_int * 4;
-  const uint32_t treebytes = (uint32_t)((size_t)A.n_int * Q * L * 4);
-  const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * A.n_int * Q * L, treebytes);
-  // inactive lanes address past the buffer: stores drop, loads return 0
-  const int voff = active ? site * 4 : 0x7FFFFFF0;
-  const int rowbytes = L * 4;
-
-  float dv[Q][SPT];
-  if constexpr (FWD) {
-    I4 nxt = load_step(prog, 0);
-    for (int k = 0; k < A.n_int; ++k) {
-      const I4 stp = nxt;
-      if (k + 1 < A.n_int) nxt = load_step(prog, k + 1);
-      // gather both children (LDS reads in flight together)
-      float d[2][Q][SPT];
-      int code[2][SPT];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int desc = c == 0 ? stp.y : stp.z;
-        const int kind = (desc >> 24) & 3;
-        if (kind == kKindLeaf) {
-          ld_codes<SPT>(lleaf + ((desc & 0xFFFF) * kWave + lane) * SPT, code[c]);
-          if constexpr (LFAST) {
-#pragma unroll
-            for (int s = 0; s < SPT; ++s) {
-              float r[Q];
-              lds_vec_get<Q>(tab + code[c][s] * Q, r);
-#pragma unroll
-              for (int i = 0; i < Q; ++i) d[c][i][s] = r[i];  // already the message
-            }
-          } else {
-#pragma unroll
-            for (int j = 0; j < Q; ++j)
-#pragma unroll
-              for (int s = 0; s < SPT; ++s)
-                d[c][j][s] = (code[c][s] == j) ? 0.0f : kSentinel;
-          }
-        } else {
-          lds_get<Q, SPT>(slots, kind == kKindInt ? ((desc >> 16) & 0xFF) : kSentSlot, lane, d[c]);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int desc = c == 0 ? stp.y : stp.z;
-        float m[Q][SPT];
-        if (LFAST && ((desc >> 24) & 3) == kKindLeaf) {
-#pragma unroll
-          for (int i = 0; i < Q; ++i)
-#pragma unroll
-            for (int s = 0; s < SPT; ++s) m[i][s] = d[c][i][s];
-        } else {
-          message<Q, SPT, MODE>(cf, a, bcoef, d[c], m);
-        }
-#pragma unroll
-        for (int i = 0; i < Q; ++i)
-#pragma unroll
-          for (int s = 0; s < SPT; ++s) dv[i][s] = (c == 0) ? m[i][s] : dv[i][s] + m[i][s];
-      }
-      const int row = stp.x & 0xFFFF;
-      const int oslot = (stp.x >> 16) & 0xFF;
-#pragma unroll
-      for (int i = 0; i < Q; ++i) bst<SPT>(rdp, voff, (row * Q + i) * rowbytes, dv[i]);
-      if (oslot != 0xFF) lds_put<Q, SPT>(slots, oslot, lane, dv);
-    }
-  } else {
-    // adjoint only: the root row comes from the table
-#pragma unroll
-    for (int i = 0; i < Q; ++i) bld<SPT>(rdp, voff, ((A.n_int - 1) * Q + i) * rowbytes, dv[i]);
-  }
-
-  // ---- root: score + cotangent ----
-  float score[SPT], groot[Q][SPT];
-  root_score<Q, SPT, SOFT>(dv, a, bcoef, A.hard_root != 0, score, groot);
-  double tot = 0.0;
-  if constexpr (FWD) {
-    if (active) {
-#pragma unroll
-      for (int s = 0; s < SPT; ++s) tot += (double)score[s];
-      if (A.site_score) st<SPT>(A.site_score + (size_t)tree * L + site, score);
-    }
-    tot = wave_sum(tot);
-  }
-
-  // acc: dC accumulators (in the factored form x K[i][j] at the end; leaf
-  // one-hot contributions are pre-divided by K via the IK table)
-  float acc[Q][Q];
-  if constexpr (BWD) {
-    const float dscale = A.dts ? as_const(A.dts)[tree] : 1.0f;
-    const float f = active ? dscale : 0.0f;
+    for (int j = 0; j < Q; ++j) d1[j][0] = kSentinel;
+    message<Q, 1, MODE>(cf, a, bcoef, d1, m1);
 #pragma unroll
     for (int i = 0; i < Q; ++i)
+      if (i == lane) tab[Q * Q + i] = m1[i][0];
 #pragma unroll
-      for (int s = 0; s < SPT; ++s) groot[i][s] *= f;
-#pragma unroll
-    for (int i = 0; i < Q; ++i)
-#pragma unroll
-      for (int j = 0; j < Q; ++j) acc[i][j] = 0.0f;
-    const bool want_marg = A.marg != nullptr;
-    const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * A.n_int * Q * L : A.dp,
-                                 treebytes);
-    int8_t* at = A.anc ? A.anc + (size_t)tree * A.n_int * L + sc : nullptr;
+    for (int st_ = 0; st_ < Q; ++st_) {
+      const float cv = as_const(A.cost)[lane * Q + st_];
+      tab[st_ * Q + lane] = cv;
+      if constexpr (MODE == kSoftK) tab[32 + st_ * Q + lane] = fast_exp2((cv - cf.cmin) * a);
+    }
+  }
 
-    // software pipeline: DP rows of the next step's internal children in flight
-    float nd[2][Q][SPT];
-    I4 nstp = load_step(prog, A.n_int - 1);
-    auto prefetch = [&](const I4& s2) {
+  // leaf-tile prefetch: lane l loads dword (l & 15) of rows 4r + (l >> 4),
+  // i.e. 16 loads cover 64 leaf rows of a 64-site tile (4-byte aligned rows)
+  // only the forward kernel loops over items: the adjoint's register
+  // footprint is too large to keep a second tile in flight
+  constexpr bool PERSIST = PHASE == 1;
+  const bool pf = PERSIST && SPT == 1 && (L & 3) == 0 && A.nl <= kPrefetchRows;
+  const int pf_voff = (lane >> 4) * L + (lane & 15) * 4;
+  uint32_t pre[kPrefetchRows / 4];
+  auto issue_prefetch = [&](int it) {
+    const int tr = it / A.tiles;
+    const int tl = it - tr * A.tiles;
+    const rsrc_t rl = make_rsrc(A.leaves + (size_t)tr * A.nl * L, (uint32_t)((size_t)A.nl * L));
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int desc = c == 0 ? s2.y : s2.z;
-        if (((desc >> 24) & 3) == kKindInt) {
-          const int crow = desc & 0xFFFF;
+    for (int r = 0; r < kPrefetchRows / 4; ++r)
+      pre[r] = __builtin_amdgcn_raw_buffer_load_b32(rl, pf_voff, 4 * r * L + tl * kWave, 0);
+  };
+  auto store_prefetch = [&]() {
+    uint32_t* dst = reinterpret_cast<uint32_t*>(lleaf);
 #pragma unroll
-          for (int j = 0; j < Q; ++j) bld<SPT>(rdp, voff, (crow * Q + j) * rowbytes, nd[c][j]);
-        }
+    for (int r = 0; r < kPrefetchRows / 4; ++r) {
+      const int row = 4 * r + (lane >> 4);
+      if (row < A.nl) dst[row * 16 + (lane & 15)] = pre[r];
+    }
+  };
+  if (pf) issue_prefetch(item);
+  __syncthreads();  // the table is written by lanes < Q, read by all
+
+  do {
+    // per-item values must not be hoisted out of this (short) loop: the
+    // laundered lane id and LDS bases keep LICM from pinning registers
+    int lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));
+    float* tab = lds;
+    asm volatile("" : "+s"(tab));
+    float* slots = tab + kTabFloats;
+    int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT);
+    const int tree = item / A.tiles;
+    const int tile = item - tree * A.tiles;
+    const int site = (tile * kWave + lane) * SPT;
+    const bool active = site < L;
+    const int sc = active ? site : 0;
+
+    // ---- leaf tile of this item ----
+    if (pf) {
+      store_prefetch();
+      if (item + stride < item_end) issue_prefetch(item + stride);
+    } else {
+      const int8_t* lv = A.leaves + (size_t)tree * A.nl * L + sc;
+      constexpr int kBatch = 8;
+      for (int c0 = 0; c0 < A.nl; c0 += kBatch) {
+        int code[kBatch][SPT];
+        const int nb_ = min(kBatch, A.nl - c0);
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u)
+          if (u < nb_) ld_codes<SPT>(lv + (size_t)(c0 + u) * L, code[u]);
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u)
+          if (u < nb_) st_codes<SPT>(lleaf + ((c0 + u) * kWave + lane) * SPT, code[u]);
       }
+    }
+
+    const cptr<int> prog = as_const(reinterpret_cast<const int*>(A.steps)) + (size_t)tree * A.n_int * 4;
+    const uint32_t treebytes = (uint32_t)((size_t)A.n_int * Q * L * 4);
+    const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * A.n_int * Q * L, treebytes);
+    // inactive lanes address past the buffer: stores drop, loads return 0
+    const int voff = active ? site * 4 : 0x7FFFFFF0;
+    const int rowbytes = L * 4;
+
+    auto child_code = [&](int desc, int (&code)[SPT]) {
+      ld_codes<SPT>(lleaf + ((desc & 0xFFFF) * kWave + lane) * SPT, code);
+#pragma unroll
+      for (int s = 0; s < SPT; ++s) code[s] = ((unsigned)code[s] < (unsigned)Q) ? code[s] : Q;
     };
-    lds_put<Q, SPT>(slots, kRootSlot, lane, groot);
-    prefetch(nstp);
-    for (int k = A.n_int - 1; k >= 0; --k) {
-      const I4 stp = nstp;
-      float cd[2][Q][SPT];
+
+    float dv[Q][SPT];
+    if constexpr (FWD) {
+      I4 nxt = load_step(prog, 0);
+      for (int k = 0; k < A.n_int; ++k) {
+        const I4 stp = nxt;
+        if (k + 1 < A.n_int) nxt = load_step(prog, k + 1);
+        // gather both children (LDS reads in flight together)
+        float d[2][Q][SPT];
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int j = 0; j < Q; ++j)
-#pragma unroll
-          for (int s = 0; s < SPT; ++s) cd[c][j][s] = nd[c][j][s];
-      if (k > 0) {
-        nstp = load_step(prog, k - 1);
-        prefetch(nstp);
-      }
-      if (stp.w & kStepUnreached) continue;
-      const int row = stp.x & 0xFFFF;
-      float g[Q][SPT];
-      lds_get<Q, SPT>(slots, (stp.w & kStepRoot) ? kRootSlot : ((stp.x >> 16) & 0xFF), lane, g);
-      int code[2][SPT];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int desc = c == 0 ? stp.y : stp.z;
-        const int kind = (desc >> 24) & 3;
-        if (kind == kKindLeaf) {
-          ld_codes<SPT>(lleaf + ((desc & 0xFFFF) * kWave + lane) * SPT, code[c]);
-        } else if (kind != kKindInt) {
-          lds_get<Q, SPT>(slots, kSentSlot, lane, cd[c]);
-        }
-      }
-      if (want_marg) {
-#pragma unroll
-        for (int i = 0; i < Q; ++i) bst<SPT>(rmg, voff, (row * Q + i) * rowbytes, g[i]);
-      }
-      if (at && active) {
-        int best[SPT];
-#pragma unroll
-        for (int s = 0; s < SPT; ++s) {
-          float bv = g[0][s];
-          int bi = 0;
-#pragma unroll
-          for (int i = 1; i < Q; ++i)
-            if (g[i][s] > bv) { bv = g[i][s]; bi = i; }
-          best[s] = bi;
-        }
-        st_codes<SPT>(at + (size_t)row * L, best);
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int desc = c == 0 ? stp.y : stp.z;
-        const int kind = (desc >> 24) & 3;
-        bool onehot = false;
-        if (kind == kKindLeaf) {
-          if constexpr (LFAST) {
-            bool miss = false;
-#pragma unroll
-            for (int s = 0; s < SPT; ++s) miss |= code[c][s] == Q;
-            onehot = !__any(miss);
-          }
-          if (!onehot) {
-#pragma unroll
-            for (int j = 0; j < Q; ++j)
-#pragma unroll
-              for (int s = 0; s < SPT; ++s)
-                cd[c][j][s] = (code[c][s] == j) ? 0.0f : kSentinel;
-          }
-        }
-        if (onehot) {
-          // exact leaf weights are one-hot: dC[i][code] += g_i
-#pragma unroll
-          for (int s = 0; s < SPT; ++s) {
-            float oh[Q], t[Q];
-#pragma unroll
-            for (int j = 0; j < Q; ++j) oh[j] = (code[c][s] == j) ? 1.0f : 0.0f;
-            if constexpr (MODE == kSoftK) {
-              float ik[Q];
-              lds_vec_get<Q>(tab + 32 + code[c][s] * Q, ik);
-#pragma unroll
-              for (int i = 0; i < Q; ++i) t[i] = g[i][s] * ik[i];
+        for (int c = 0; c < 2; ++c) {
+          const int desc = c == 0 ? stp.y : stp.z;
+          const int kind = (desc >> 24) & 3;
+          if (kind == kKindInt) {
+            lds_get<Q, SPT>(slots, (desc >> 16) & 0xFF, lane, d[c]);
+          } else {
+            int code[SPT];
+            if (kind == kKindLeaf) {
+              child_code(desc, code);
             } else {
 #pragma unroll
-              for (int i = 0; i < Q; ++i) t[i] = g[i][s];
+              for (int s = 0; s < SPT; ++s) code[s] = Q;  // all-1e5 row
             }
+            if constexpr (LFAST) {
 #pragma unroll
-            for (int i = 0; i < Q; ++i)
+              for (int s = 0; s < SPT; ++s) {
+                float r[Q];
+                lds_vec_get<Q>(tab + code[s] * Q, r);
 #pragma unroll
-              for (int j = 0; j < Q; ++j) acc[i][j] = fmaf(t[i], oh[j], acc[i][j]);
-          }
-        } else {
-          float gc[Q][SPT];
-          message_adjoint<Q, SPT, MODE>(cf, a, cd[c], g, acc, gc);
-          if (kind == kKindInt) {
-            const int cslot = (desc >> 16) & 0xFF;
-            if (desc & kStepAccumulate) {
-              float old[Q][SPT];
-              lds_get<Q, SPT>(slots, cslot, lane, old);
+                for (int i = 0; i < Q; ++i) d[c][i][s] = r[i];  // already the message
+              }
+            } else {
 #pragma unroll
               for (int j = 0; j < Q; ++j)
 #pragma unroll
-                for (int s = 0; s < SPT; ++s) gc[j][s] += old[j][s];
+                for (int s = 0; s < SPT; ++s) d[c][j][s] = (code[s] == j) ? 0.0f : kSentinel;
             }
-            lds_put<Q, SPT>(slots, cslot, lane, gc);
           }
         }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int desc = c == 0 ? stp.y : stp.z;
+          float m[Q][SPT];
+          if (LFAST && ((desc >> 24) & 3) != kKindInt) {
+#pragma unroll
+            for (int i = 0; i < Q; ++i)
+#pragma unroll
+              for (int s = 0; s < SPT; ++s) m[i][s] = d[c][i][s];
+          } else {
+            message<Q, SPT, MODE>(cf, a, bcoef, d[c], m);
+          }
+#pragma unroll
+          for (int i = 0; i < Q; ++i)
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) dv[i][s] = (c == 0) ? m[i][s] : dv[i][s] + m[i][s];
+        }
+        const int row = stp.x & 0xFFFF;
+        const int oslot = (stp.x >> 16) & 0xFF;
+#pragma unroll
+        for (int i = 0; i < Q; ++i) bst<SPT>(rdp, voff, (row * Q + i) * rowbytes, dv[i]);
+        if (oslot != 0xFF) lds_put<Q, SPT>(slots, oslot, lane, dv);
       }
+    } else {
+      // adjoint only: the root row comes from the table
+#pragma unroll
+      for (int i = 0; i < Q; ++i) bld<SPT>(rdp, voff, ((A.n_int - 1) * Q + i) * rowbytes, dv[i]);
     }
-  }
 
-  // ---- epilogue: deterministic two-level reduction, last block finishes ----
-  const int nb = A.B * A.tiles;
-  double dsum[Q * Q];
-  if constexpr (BWD) {
+    // ---- root: score + cotangent ----
+    float score[SPT], groot[Q][SPT];
+    root_score<Q, SPT, SOFT>(dv, a, bcoef, A.hard_root != 0, score, groot);
+    if constexpr (FWD) {
+      double tot = 0.0;
+      if (active) {
 #pragma unroll
-    for (int i = 0; i < Q; ++i)
-#pragma unroll
-      for (int j = 0; j < Q; ++j) {
-        double v = (double)acc[i][j];
-        if constexpr (MODE == kSoftK) v = v * (double)cf.k[i][j];
-        dsum[i * Q + j] = wave_sum(v);
+        for (int s = 0; s < SPT; ++s) tot += (double)score[s];
+        if (A.site_score) st<SPT>(A.site_score + (size_t)tree * L + site, score);
       }
-  }
-  if (lane == 0) {
-    if (FWD) store_sc1(A.part_tree + blockIdx.x, tot);
-    if (BWD) {
+      tot = wave_sum(tot);
+      if (lane == 0) A.part_tree[item] = tot;
+    }
+
+    if constexpr (BWD) {
+      // acc: dC accumulators (in the factored form x K[i][j] at the end; leaf
+      // one-hot contributions are pre-divided by K via the IK table)
+      float acc[Q][Q];
+      const float dscale = A.dts ? as_const(A.dts)[tree] : 1.0f;
+      const float f = active ? dscale : 0.0f;
 #pragma unroll
-      for (int q = 0; q < Q * Q; ++q) store_sc1(A.part_dc + (size_t)q * nb + blockIdx.x, dsum[q]);
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int s = 0; s < SPT; ++s) groot[i][s] *= f;
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int j = 0; j < Q; ++j) acc[i][j] = 0.0f;
+      const bool want_marg = A.marg != nullptr;
+      const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * A.n_int * Q * L : A.dp,
+                                   treebytes);
+      int8_t* at = A.anc ? A.anc + (size_t)tree * A.n_int * L + sc : nullptr;
+      lds_put<Q, SPT>(slots, kRootSlot, lane, groot);
+
+      // DP rows of a step's internal children are loaded one step ahead into
+      // the other half of a ping-pong buffer (the loop is unrolled by two so
+      // the prefetched registers are consumed in place, never copied -- a
+      // copy would force a vmcnt(0) wait at the back edge).  The loads are
+      // unconditional (non-internal children read past the buffer: no
+      // memory traffic, zeros) so every path issues the same number of VMEM
+      // ops and the compiler's vmcnt waits stay partial.
+      auto prefetch = [&](const I4& s2, float (&nd)[2][Q][SPT]) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int desc = c == 0 ? s2.y : s2.z;
+          const bool internal = ((desc >> 24) & 3) == kKindInt;
+          const int vo = internal ? voff : 0x7FFFFFF0;
+          const int crow = internal ? (desc & 0xFFFF) : 0;
+#pragma unroll
+          for (int j = 0; j < Q; ++j) bld<SPT>(rdp, vo, (crow * Q + j) * rowbytes, nd[c][j]);
+        }
+      };
+      auto bstep = [&](const I4& stp, float (&cd)[2][Q][SPT]) {
+        if (stp.w & kStepUnreached) return;
+        const int row = stp.x & 0xFFFF;
+        float g[Q][SPT];
+        lds_get<Q, SPT>(slots, (stp.w & kStepRoot) ? kRootSlot : ((stp.x >> 16) & 0xFF), lane, g);
+        if (want_marg) {
+#pragma unroll
+          for (int i = 0; i < Q; ++i) bst<SPT>(rmg, voff, (row * Q + i) * rowbytes, g[i]);
+        }
+        if (at && active) {
+          int best[SPT];
+#pragma unroll
+          for (int s = 0; s < SPT; ++s) {
+            float bv = g[0][s];
+            int bi = 0;
+#pragma unroll
+            for (int i = 1; i < Q; ++i)
+              if (g[i][s] > bv) { bv = g[i][s]; bi = i; }
+            best[s] = bi;
+          }
+          st_codes<SPT>(at + (size_t)row * L, best);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int desc = c == 0 ? stp.y : stp.z;
+          const int kind = (desc >> 24) & 3;
+          int code[SPT];
+          bool onehot = false;
+          if (kind == kKindLeaf) {
+            child_code(desc, code);
+            if constexpr (LFAST) {
+              bool miss = false;
+#pragma unroll
+              for (int s = 0; s < SPT; ++s) miss |= code[s] == Q;
+              onehot = !__any(miss);
+            }
+            if (!onehot) {
+#pragma unroll
+              for (int j = 0; j < Q; ++j)
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) cd[c][j][s] = (code[s] == j) ? 0.0f : kSentinel;
+            }
+          } else if (kind != kKindInt) {
+            fill_sentinel<Q, SPT>(cd[c]);
+          }
+          if (onehot) {
+            // exact leaf weights are one-hot: dC[i][code] += g_i
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+              float oh[Q], t[Q];
+#pragma unroll
+              for (int j = 0; j < Q; ++j) oh[j] = (code[s] == j) ? 1.0f : 0.0f;
+              if constexpr (MODE == kSoftK) {
+                float ik[Q];
+                lds_vec_get<Q>(tab + 32 + code[s] * Q, ik);
+#pragma unroll
+                for (int i = 0; i < Q; ++i) t[i] = g[i][s] * ik[i];
+              } else {
+#pragma unroll
+                for (int i = 0; i < Q; ++i) t[i] = g[i][s];
+              }
+#pragma unroll
+              for (int i = 0; i < Q; ++i) axpy<Q>(acc[i], t[i], oh);
+            }
+          } else {
+            float gc[Q][SPT];
+            message_adjoint<Q, SPT, MODE>(cf, a, cd[c], g, acc, gc);
+            if (kind == kKindInt) {
+              const int cslot = (desc >> 16) & 0xFF;
+              if (desc & kStepAccumulate) {
+                float old[Q][SPT];
+                lds_get<Q, SPT>(slots, cslot, lane, old);
+#pragma unroll
+                for (int j = 0; j < Q; ++j)
+#pragma unroll
+                  for (int s = 0; s < SPT; ++s) gc[j][s] += old[j][s];
+              }
+              lds_put<Q, SPT>(slots, cslot, lane, gc);
+            }
+          }
+        }
+      };
+      float bufA[2][Q][SPT], bufB[2][Q][SPT];
+      I4 sA = load_step(prog, A.n_int - 1);
+      I4 sB = A.n_int > 1 ? load_step(prog, A.n_int - 2) : sA;
+      const I4 none = {0, 0, 0, 0};  // sentinel children only: prefetch reads nothing
+      prefetch(sA, bufA);
+      for (int k = A.n_int - 1; k >= 0; k -= 2) {
+        // step k uses A while B fills for step k-1
+        prefetch(k >= 1 ? sB : none, bufB);
+        const I4 cA = sA;
+        if (k >= 2) sA = load_step(prog, k - 2);
+        bstep(cA, bufA);
+        if (k < 1) break;
+        // step k-1 uses B while A fills for step k-2
+        prefetch(k >= 2 ? sA : none, bufA);
+        const I4 cB = sB;
+        if (k >= 3) sB = load_step(prog, k - 3);
+        bstep(cB, bufB);
+      }
+
+      // ---- per-item dC partial (fixed-order reduce kernel sums the items) ----
+#pragma unroll
+      for (int i = 0; i < Q; ++i)
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+          double v = (double)acc[i][j];
+          if constexpr (MODE == kSoftK) v = v * (double)cf.k[i][j];
+          v = wave_sum(v);
+          if (lane == 0) A.part_dc[(size_t)(i * Q + j) * nb + item] = v;
+        }
     }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int old = 0;
-  if (lane == 0)
-    old = __hip_atomic_fetch_add(A.counters + tree, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = __shfl(old, 0, kWave);
-  if (old != A.tiles - 1) return;
-  // last tile of this tree
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (lane == 0) __hip_atomic_store(A.counters + tree, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const size_t t0 = (size_t)tree * A.tiles;
-  if constexpr (FWD) {
-    const double s = wave_sum_strided(A.part_tree + t0, A.tiles, lane);
-    if (lane == 0) A.tree_score[tree] = (float)s;
-  }
-  if constexpr (BWD) {
-    for (int q = 0; q < Q * Q; ++q) {
-      const double s = wave_sum_strided(A.part_dc + (size_t)q * nb + t0, A.tiles, lane);
-      if (lane == 0) store_sc1(A.tree_dc + (size_t)q * A.B + tree, s);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int old2 = 0;
-    if (lane == 0)
-      old2 = __hip_atomic_fetch_add(A.counters + A.B, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old2 = __shfl(old2, 0, kWave);
-    if (old2 != A.B - 1) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (lane == 0) __hip_atomic_store(A.counters + A.B, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int q = 0; q < Q * Q; ++q) {
-      const double s = wave_sum_strided(A.tree_dc + (size_t)q * A.B, A.B, lane);
-      if (lane == 0) A.d_cost[q] = (float)s;
-    }
-  }
+    item += stride;
+  } while (PERSIST && item < item_end);
 }
 
 template <int Q, int SPT, int MODE, int PHASE>
@@ -817,7 +861,8 @@ __device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds
 }
 
 template <int Q, int SPT, bool SOFT, int PHASE>
-__global__ __launch_bounds__(kWave) void sankoff_kernel(KArgs A) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? 6 : 5, 8)))
+void sankoff_kernel(KArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if constexpr (!SOFT) {
     sankoff_dispatch_leaf<Q, SPT, kHard, PHASE>(A, lds);
@@ -960,20 +1005,20 @@ int check_shape(const char* fn, int B, int L, int n_all, int Q, Shape* sh) {
 int tiles_for(int L, int spt) { return (L + kWave * spt - 1) / (kWave * spt); }
 
 size_t lds_bytes(int n_slots, int nl, int Q, int spt) {
-  const size_t b = (size_t)kTabFloats * 4 + (size_t)(n_slots + 2) * Q * kWave * spt * 4 +
+  const size_t b = (size_t)kTabFloats * 4 + (size_t)(n_slots + 1) * Q * kWave * spt * 4 +
                    (size_t)nl * kWave * spt;
   return (b + 15) & ~(size_t)15;
 }
 
-// sites per lane: 2 when L is even and the wave's LDS (stack + leaf tile)
-// stays <= 12 KiB, else 1.  TREX_SPT=1|2 overrides (tuning).
+// sites per lane: 1 (measured fastest for the fused soft kernel: SPT=2
+// doubles the adjoint's VGPRs and halves occupancy).  TREX_SPT=2 forces two
+// sites per lane when L is even and the stack fits 12 KiB (tuning).
 int pick_spt(int L, int n_slots, int nl, int Q) {
   static const int forced = [] {
     const char* e = std::getenv("TREX_SPT");
     return e ? std::atoi(e) : 0;
   }();
-  if ((forced == 1 || forced == 2) && L % forced == 0) return forced;
-  if (L % 2 == 0 && lds_bytes(n_slots, nl, Q, 2) <= 12288) return 2;
+  if (forced == 2 && L % 2 == 0 && lds_bytes(n_slots, nl, Q, 2) <= 12288) return 2;
   return 1;
 }
 
@@ -995,25 +1040,64 @@ void tau_coefs(float tau, float* a, float* bcoef) {
   }
 }
 
+// persistent grid: as many single-wave blocks as are co-resident (occupancy
+// x CUs), a multiple of 8 (one share per XCD), never more than the items
+template <class K>
+int persistent_grid(K kernel, size_t lds, int nitems) {
+  static std::mutex mu;
+  static int cus = 0;
+  struct Entry { const void* k; size_t lds; int occ; };
+  static Entry cache[64];
+  static int ncache = 0;
+  int occ = 0;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    if (cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    }
+    for (int i = 0; i < ncache; ++i)
+      if (cache[i].k == (const void*)kernel && cache[i].lds == lds) occ = cache[i].occ;
+    if (occ == 0) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kWave, lds) != hipSuccess ||
+          occ <= 0)
+        occ = 4;
+      if (ncache < 64) cache[ncache++] = Entry{(const void*)kernel, lds, occ};
+    }
+  }
+  static const int persist = [] {
+    const char* e = std::getenv("TREX_PERSIST");
+    return e ? std::atoi(e) : 1;
+  }();
+  const long resident = persist ? (long)cus * occ / 8 * 8 : (1L << 30);
+  const long want = ((long)nitems + 7) / 8 * 8;
+  return (int)std::max(8L, std::min(resident, want));
+}
+
 template <int Q, int SPT, bool SOFT>
-void launch_phase(int phase, int grid, size_t lds, hipStream_t st, const KArgs& A) {
+void launch_phase(int phase, size_t lds, hipStream_t st, const KArgs& A) {
+  auto go = [&](auto kernel) {
+    const int grid = phase == 1 ? persistent_grid(kernel, lds, A.nblocks) : (A.nblocks + 7) / 8 * 8;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWave), lds, st, A);
+  };
   if (phase == 1)
-    hipLaunchKernelGGL((sankoff_kernel<Q, SPT, SOFT, 1>), dim3(grid), dim3(kWave), lds, st, A);
+    go(sankoff_kernel<Q, SPT, SOFT, 1>);
   else if (phase == 2)
-    hipLaunchKernelGGL((sankoff_kernel<Q, SPT, SOFT, 2>), dim3(grid), dim3(kWave), lds, st, A);
+    go(sankoff_kernel<Q, SPT, SOFT, 2>);
   else
-    hipLaunchKernelGGL((sankoff_kernel<Q, SPT, SOFT, 3>), dim3(grid), dim3(kWave), lds, st, A);
+    go(sankoff_kernel<Q, SPT, SOFT, 3>);
 }
 
 template <int Q>
-void dispatch_q(int phase, int spt, bool soft, int grid, size_t lds, hipStream_t st,
-                const KArgs& A) {
+void dispatch_q(int phase, int spt, bool soft, size_t lds, hipStream_t st, const KArgs& A) {
   if (spt == 2) {
-    if (soft) launch_phase<Q, 2, true>(phase, grid, lds, st, A);
-    else launch_phase<Q, 2, false>(phase, grid, lds, st, A);
+    if (soft) launch_phase<Q, 2, true>(phase, lds, st, A);
+    else launch_phase<Q, 2, false>(phase, lds, st, A);
   } else {
-    if (soft) launch_phase<Q, 1, true>(phase, grid, lds, st, A);
-    else launch_phase<Q, 1, false>(phase, grid, lds, st, A);
+    if (soft) launch_phase<Q, 1, true>(phase, lds, st, A);
+    else launch_phase<Q, 1, false>(phase, lds, st, A);
   }
 }
 
@@ -1103,24 +1187,20 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   A.marg = marg;
   A.anc = anc;
   A.d_cost = d_cost;
-  char* w = static_cast<char*>(workspace);
-  const int64_t nbmax = (int64_t)B * tiles_for(L, 1);
-  A.counters = reinterpret_cast<int*>(w);
-  w += counters_bytes(B);
+  // workspace: per-item partials [B*tiles] + [Q*Q][B*tiles] doubles
+  char* w = static_cast<char*>(workspace) + counters_bytes(B);
   A.part_tree = reinterpret_cast<double*>(w);
-  w += nbmax * 8;
-  A.part_dc = reinterpret_cast<double*>(w);
-  w += nbmax * 8 * Q * Q;
-  A.tree_dc = reinterpret_cast<double*>(w);
+  A.nblocks = B * tiles;
+  A.part_dc = A.part_tree + A.nblocks;
   const bool soft = tau > 0.0f;
   hipStream_t st = (hipStream_t)stream;
-  const int grid = B * tiles;
   switch (Q) {
-    case 2: dispatch_q<2>(phase, spt, soft, grid, lds, st, A); break;
-    case 3: dispatch_q<3>(phase, spt, soft, grid, lds, st, A); break;
-    case 4: dispatch_q<4>(phase, spt, soft, grid, lds, st, A); break;
+    case 2: dispatch_q<2>(phase, spt, soft, lds, st, A); break;
+    case 3: dispatch_q<3>(phase, spt, soft, lds, st, A); break;
+    case 4: dispatch_q<4>(phase, spt, soft, lds, st, A); break;
   }
-  return hip_check(fn);
+  if (int e = hip_check(fn)) return e;
+  return partial_reduce(fn, A.part_tree, A.part_dc, B, tiles, Q, phase, tree_score, d_cost, stream);
 }
 
 }  // namespace

@@ -472,8 +472,9 @@ __global__ __launch_bounds__(kWave) void sankoff_wide_kernel(WArgs A) {
   }
 }
 
-// fixed-order reduction of the per-wave partials: blocks [0, B) = tree
-// scores, blocks [B, B + Q*Q) = dC entries
+// fixed-order reduction of per-item partials (both Sankoff paths): blocks
+// [0, B) = tree scores, blocks [B, B + Q*Q) = dC entries; bitwise
+// reproducible, and no arrival counters, so launches replay in hipGraphs
 __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restrict__ part_tree,
                                                           const double* __restrict__ part_dc,
                                                           int B, int tiles, int Q2, int do_tree,
@@ -633,11 +634,19 @@ int wide_run(const char* fn, const WideCall& c) {
     case 20: launch_wide_g<20>(c.phase, c.soft, grid, lds, st, A); break;
     default: launch_wide_g<32>(c.phase, c.soft, grid, lds, st, A); break;
   }
-  const bool do_tree = (c.phase & 1) != 0;
-  const bool do_dc = (c.phase & 2) != 0;
-  const int rgrid = (do_tree ? c.B : 0) + (do_dc ? c.Q * c.Q : 0);
-  hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(256), 0, st, A.part_tree, A.part_dc,
-                     c.B, tiles, c.Q * c.Q, do_tree ? 1 : 0, c.tree_score, c.d_cost);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return partial_reduce(fn, A.part_tree, A.part_dc, c.B, tiles, c.Q, c.phase, c.tree_score,
+                        c.d_cost, c.stream);
+}
+
+int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
+                   int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream) {
+  const bool do_tree = (phase & 1) != 0;
+  const bool do_dc = (phase & 2) != 0;
+  const int rgrid = (do_tree ? B : 0) + (do_dc ? Q * Q : 0);
+  hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(256), 0, (hipStream_t)stream,
+                     part_tree, part_dc, B, tiles, Q * Q, do_tree ? 1 : 0, tree_score, d_cost);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
   return TREX_OK;
