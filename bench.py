@@ -217,8 +217,9 @@ def c3_line(torch, device, cpu_threads):
     torch.cuda.synchronize()
     k_s = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev])) * 1e-3
     units = L * n_int * Q
-    # algorithmic bytes: leaves in, dp + marginals out (f32), anc states out (i8)
-    abytes = L * (nl + 8 * Q * n_int + n_int)
+    # algorithmic bytes (SURVEY.md 8(d) fwd+grad + C3 extras): leaves in twice,
+    # DP table out + adjoint re-read, marginals out (f32), anc states out (i8)
+    abytes = L * (2 * nl + 8 * Q * n_int + 4 * Q * n_int + n_int)
     res = {"workload": "C3: balanced 64-taxa tree x 10000 sites x 20 states, softmin tau=0.5 "
                        "fwd+grad+marginals+soft ancestral (fused) | hard fwd + trex backtrack",
            "soft_ms_per_step": soft_s * 1e3, "soft_value": units / soft_s,
@@ -386,29 +387,36 @@ def main():
     # per-kernel device time (HIP events) -> roofline of the step's kernel
     kt = time_kernels(torch, step)
     nl = n
-    # algorithmic HBM bytes per launch (DESIGN.md "Roofline"):
-    #   fused: int8 leaves in + fp32 DP table out (its re-read is a cache-
-    #          resident recompute choice, not algorithmic traffic)
-    #   fwd:   leaves in + DP table out;  bwd: leaves + DP table in
+    # algorithmic HBM bytes per launch, SURVEY.md section 8(d) / DESIGN.md "Roofline":
+    #   fwd:   int8 leaves in + fp32 DP table out            B*L*(n + 4*Q*n_int)
+    #   bwd:   leaves + DP table in                          B*L*(n + 4*Q*n_int)
+    #   fused: fwd + the adjoint's re-read of both           B*L*(2n + 8*Q*n_int)
+    #   (no site scores are written in this step; dC and tree scores are O(Q^2 + B))
     fwd_bytes = B * L * (nl + 4 * Q * n_int)
-    kern = {"sankoff_fwd_bwd": (kt["sankoff_fwd_bwd"], fwd_bytes),
+    kern = {"sankoff_fwd_bwd": (kt["sankoff_fwd_bwd"], 2 * fwd_bytes),
             "sankoff_fwd": (kt["sankoff_fwd"], fwd_bytes),
             "sankoff_bwd": (kt["sankoff_bwd"], fwd_bytes)}
     dom = "sankoff_fwd_bwd"
     achieved = kern[dom][1] / kern[dom][0] / 1e9
-    traffic = None
+    # measured HBM traffic per launch (rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
+    # calibrated: tools/traffic_passes.sh -> profiles/traffic.json)
+    traffic = {}
     try:
         with open(args.traffic) as f:
             tj = json.load(f)
         if tj.get("workload_key") == f"{B}x{n}x{L}x{Q}":
-            traffic = tj.get(dom)
+            traffic = {k: tj.get(k) for k in kern}
     except (OSError, ValueError):
         pass
+    per_kernel = {k: {"us": round(v[0] * 1e6, 2), "algorithmic_bytes": v[1],
+                      "GBs": round(v[1] / v[0] / 1e9, 1),
+                      "frac": round(v[1] / v[0] / 1e9 / HBM_PEAK_GBS, 4),
+                      "traffic_bytes": traffic.get(k)} for k, v in kern.items()}
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "per_kernel_us": {k: round(v[0] * 1e6, 2) for k, v in kern.items()},
-                "algorithmic_bytes": {k: v[1] for k, v in kern.items()}}
+                "traffic": traffic.get(dom),
+                "per_kernel": per_kernel,
+                "per_kernel_us": {k: round(v[0] * 1e6, 2) for k, v in kern.items()}}
 
     result = {
         "metric": "site-node-state updates/sec (Sankoff fwd+grad)",

@@ -496,9 +496,16 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
     n = (int)nb;
     dst = d_cost + q;
   }
-  double v = 0.0;
-  for (int t = threadIdx.x; t < n; t += 256) v += src[t];
-  red[threadIdx.x] = v;
+  // eight independent accumulators keep eight loads in flight per thread;
+  // the summation order is fixed (bitwise reproducible)
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int t = threadIdx.x;
+  for (; t + 7 * 256 < n; t += 8 * 256) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += src[t + j * 256];
+  }
+  for (; t < n; t += 256) acc[0] += src[t];
+  red[threadIdx.x] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   for (int h = 128; h > 0; h >>= 1) {
     if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
