@@ -243,45 +243,60 @@ def c3_line(torch, device, cpu_threads):
     return res
 
 
-def c5_line(torch, device, steps=20, warmup=3):
-    """C5 (BASELINE.json configs[4]) on one GPU: 256 taxa (511 nodes) x 50 000
-    sites x 4 states, joint Adam optimisation step (update_seq, update_tree,
-    surrogate + graph constraint, their VJPs, optax Adam) -- trex's
-    tests/test_convergence.py:208-261 loop at C5 size.  Eager launches (Adam's
-    bias correction changes every step)."""
+def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
+    """C5 (BASELINE.json configs[4]): 256 taxa (511 nodes) x 50 000 sites x 4
+    states, joint Adam optimisation step (update_seq, update_tree, surrogate
+    + graph constraint, their VJPs, optax Adam) -- trex's
+    tests/test_convergence.py:208-261 loop at C5 size.  With N > 1 ranks the
+    sites shard: one all-reduce of the 511 x 511 Gram per step
+    (strong scaling: the 50 000 sites are split).  Eager launches (Adam's bias
+    correction changes every step)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _cases import simulate_leaves
 
-    from trex_amd.tree import TreeOptimizer
+    from trex_amd.distributed import shard_bounds
+    from trex_amd.tree import TreeOptimizer, gumbel_noise
 
     nl, L, Q = 256, 50000, 4
     n = 2 * nl - 1
+    lo, hi = shard_bounds(L, rank, world)
     seqs, _ = simulate_leaves(nl, L, Q, 5, seed=6)
-    S = torch.zeros((n, L, Q), dtype=torch.float32, device=device)
-    S[:nl] = torch.nn.functional.one_hot(torch.as_tensor(seqs[:nl].astype(np.int64),
-                                                         device=device), Q).float()
+    S = torch.zeros((n, hi - lo, Q), dtype=torch.float32, device=device)
+    S[:nl] = torch.nn.functional.one_hot(
+        torch.as_tensor(seqs[:nl, lo:hi].astype(np.int64), device=device), Q).float()
     g = torch.Generator(device=device)
-    g.manual_seed(7)
+    g.manual_seed(7)  # identical on every rank: replicated tree params and noise
     params = {"tree_params": torch.randn((n - 1, nl - 1), generator=g, device=device),
-              "ancestors": torch.randn((nl - 1, L, Q), generator=g, device=device)}
-    from trex_amd.tree import gumbel_noise
-
+              "ancestors": torch.randn((nl - 1, L, Q), generator=g, device=device)[:, lo:hi]
+              .contiguous()}
     noise = [gumbel_noise((n - 1, nl - 1), generator=g, device=device) for _ in range(4)]
-    opt = TreeOptimizer(S, params, lr=0.01)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+
+        group = dist.group.WORLD
+    opt = TreeOptimizer(S, params, lr=0.01, group=group)
     for k in range(warmup):
         opt.step(max(0.1, 2.0 * (1.0 - k / 5000)), noise[k % 4])
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
     for k in range(steps):
         loss = opt.step(max(0.1, 2.0 * (1.0 - (warmup + k) / 5000)), noise[k % 4])
-    ev1.record()
     torch.cuda.synchronize()
-    sec = ev0.elapsed_time(ev1) * 1e-3 / steps
-    flops = 4.0 * n * n * L * Q  # G = S S^T and dS = M S, as trex's GEMMs
+    sec = (time.perf_counter() - t0) / steps
+    if world > 1:
+        t = torch.tensor([sec], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sec = float(t.item())
+    flops = 4.0 * n * n * L * Q  # G = S S^T and dS = M S over all sites, as trex's GEMMs
     return {"workload": "C5: 511-node relaxed tree x 50000 sites x 4 states, joint Adam step "
-                        "(surrogate + constraint + VJPs + optax adam), f32 MFMA GEMMs",
-            "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec,
+                        "(surrogate + constraint + VJPs + optax adam), f32 MFMA GEMMs"
+                        + (f"; sites sharded over {world} ranks, Gram all-reduce" if world > 1
+                           else ""),
+            "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec, "n_gpus": world,
+            "scaling": "strong" if world > 1 else None,
             "gemm_tflops": flops / sec / 1e12, "loss_last": float(loss)}
 
 
@@ -330,10 +345,16 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
-    device = torch.device("cuda", local)
+    # TREX_BENCH_DEVICE_SHARE=1 rehearses N ranks on one GPU over gloo (code
+    # path check only; timings are not meaningful); the driver's runs use RCCL
+    share = os.environ.get("TREX_BENCH_DEVICE_SHARE") == "1"
+    device = torch.device("cuda", 0 if share else local)
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     from trex_amd import SankoffEngine
 
@@ -450,6 +471,8 @@ def main():
             result["c3"] = c3_line(torch, device, threads)
         if not args.no_c5:
             result["c5"] = c5_line(torch, device)
+    if world > 1 and not args.no_c5:
+        result["c5"] = c5_line(torch, device, rank=rank, world=world)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

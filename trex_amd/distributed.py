@@ -1,4 +1,8 @@
-"""Tree-batch data parallelism: one process per GPU, trees sharded, one all-reduce.
+"""Data parallelism for the two sharded paths (one process per GPU).
+
+C4 (Sankoff): tree-batch sharding, one all-reduce of [dC, loss].
+C5 (tree cost): site sharding, one all-reduce of the N x N Gram matrix.
+
 
 Trees (and sites) are independent in Sankoff (src/trex/sankoff.py:97 vmaps
 sites; trex has no batch-of-trees axis or collectives).  The build shards
@@ -39,3 +43,25 @@ class GradReducer:
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(self.buf, group=self.group)
         return self.buf[:q2].view(self.Q, self.Q), self.buf[q2]
+
+
+class GramReducer:
+    """C5 site sharding: the surrogate's only cross-site term.
+
+    compute_surrogate_cost (src/trex/tree.py:199-209) depends on the sites only
+    through G = S S^T (with E = diag G), a sum over sites; each rank computes
+    G over its block of sites and one all-reduce (N*N fp32, 1.04 MB at
+    N = 511) makes every rank's G the full one.  The combine (value, dA,
+    M = diag(r+c) - (A+A^T)), the tree_params gradient and their Adam update
+    are then identical on all ranks; dS = M S_local stays local.
+    """
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def __call__(self, G):
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(G, group=self.group)
+        return G

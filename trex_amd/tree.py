@@ -305,6 +305,11 @@ class TreeOptimizer:
         self.n_anc = self.N - self.n_leaf
         self.scale = float(graph_constraint_scale)
         self.group = group
+        self.reducer = None
+        if group is not None:
+            from .distributed import GramReducer
+
+            self.reducer = GramReducer(group)
         if group is not None and clip_norm is not None:
             raise NotImplementedError("clip_by_global_norm with site sharding")
         f32 = dict(dtype=torch.float32, device=dev)
@@ -332,10 +337,8 @@ class TreeOptimizer:
                                        1.0, ptr(self.A), st))
         check(L_.trex_tree_gram(ptr(self.S), N, K, ptr(self.G), ptr(self.ws), self.ws.numel(),
                                 st))
-        if self.group is not None:
-            import torch.distributed as dist
-
-            dist.all_reduce(self.G, group=self.group)
+        if self.reducer is not None:
+            self.reducer(self.G)
         check(L_.trex_tree_surrogate_combine(ptr(self.A), ptr(self.G), N, ptr(self.loss),
                                              ptr(self.dA), ptr(self.M), ptr(self.ws), st))
         check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
