@@ -197,6 +197,11 @@ int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
 int trex_tree_surrogate_combine(const float* A, const float* G, int N, float* loss, float* dA,
                                 float* M, void* workspace, void* stream);
 int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS, void* stream);
+/* dS rows [row0, row0 + nrows) only (dS_rows [nrows][K]): the optimiser needs
+ * d loss / dS for the ancestor rows alone (leaf sequences are fixed,
+ * tree.py:127), which halves the MF GEMM at N = 2 n_leaf - 1. */
+int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t K, int row0, int nrows,
+                      float* dS_rows, void* stream);
 
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */

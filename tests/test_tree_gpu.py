@@ -206,3 +206,22 @@ def test_tree_optimizer_matches_oracle_loop(device):
         p_ref = {k: p_ref[k] + upd[k] for k in p_ref}
     for k in p_ref:
         np.testing.assert_allclose(_n(opt.params[k]), p_ref[k], rtol=5e-5, atol=5e-6)
+
+
+@pytest.mark.parametrize("N,K,row0", [(511, 4096, 256), (100, 132, 37), (64, 64, 0)])
+def test_mf_rows_equals_full_dS_slice(device, N, K, row0):
+    """trex_tree_mf_rows (the optimiser's ancestor-rows-only dS = M S) is
+    bit-identical to the corresponding rows of the full product."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    rng = np.random.default_rng(N + K)
+    M = _t(rng.normal(size=(N, N)), device)
+    S = _t(rng.normal(size=(N, K)), device)
+    full = torch.empty((N, K), device=device)
+    part = torch.empty((N - row0, K), device=device)
+    st = stream_handle(torch.device(device))
+    check(lib().trex_tree_mf(ptr(M), ptr(S), N, K, ptr(full), st))
+    check(lib().trex_tree_mf_rows(ptr(M), ptr(S), N, K, row0, N - row0, ptr(part), st))
+    assert torch.equal(part, full[row0:])
+    ref = _n(M).astype(np.float64) @ _n(S)
+    np.testing.assert_allclose(_n(full), ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())

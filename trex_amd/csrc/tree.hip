@@ -17,12 +17,12 @@
 #include <algorithm>
 #include <cmath>
 
+#include "sankoff_dev.h"
 #include "trex_common.h"
 
 namespace trex {
 namespace {
 
-constexpr int kWave = 64;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 int tree_hip_check(const char* fn) {
@@ -48,20 +48,30 @@ __device__ __forceinline__ double block_sum_256(double v, double* sh) {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void update_seq_kernel(const float* __restrict__ x, int64_t rows,
                                                         int Q, float T, float* __restrict__ s) {
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
-       r += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(s)) & 15) == 0;
+  if (Q == 4 && al) {  // one float4 in, one float4 out per row
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    float4* s4 = reinterpret_cast<float4*>(s);
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += stride) {
+      const float4 v = x4[r];
+      const float a = v.x * T, b = v.y * T, c = v.z * T, d = v.w * T;
+      const float m = fmaxf(fmaxf(a, b), fmaxf(c, d));
+      const float ea = expf(a - m), eb = expf(b - m), ec = expf(c - m), ed = expf(d - m);
+      const float inv = 1.0f / (((ea + eb) + ec) + ed);
+      s4[r] = make_float4(ea * inv, eb * inv, ec * inv, ed * inv);
+    }
+    return;
+  }
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += stride) {
     const float* xr = x + r * Q;
     float* sr = s + r * Q;
     float m = -INFINITY;
     for (int q = 0; q < Q; ++q) m = fmaxf(m, xr[q] * T);
     float sum = 0.0f;
-    for (int q = 0; q < Q; ++q) {
-      const float e = expf(xr[q] * T - m);
-      sr[q] = e;
-      sum += e;
-    }
+    for (int q = 0; q < Q; ++q) sum += expf(xr[q] * T - m);
     const float inv = 1.0f / sum;
-    for (int q = 0; q < Q; ++q) sr[q] *= inv;
+    for (int q = 0; q < Q; ++q) sr[q] = expf(xr[q] * T - m) * inv;  // one store per element
   }
 }
 
@@ -69,8 +79,25 @@ __global__ __launch_bounds__(256) void update_seq_bwd_kernel(const float* __rest
                                                             const float* __restrict__ ds,
                                                             int64_t rows, int Q, float T,
                                                             float* __restrict__ dx) {
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
-       r += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool al = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(ds) |
+                    reinterpret_cast<uintptr_t>(dx)) & 15) == 0;
+  if (Q == 4 && al) {
+    const float4* s4 = reinterpret_cast<const float4*>(s);
+    const float4* g4 = reinterpret_cast<const float4*>(ds);
+    float4* d4 = reinterpret_cast<float4*>(dx);
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += stride) {
+      const float4 a = s4[r], g = g4[r];
+      float dot = a.x * g.x;
+      dot = fmaf(a.y, g.y, dot);
+      dot = fmaf(a.z, g.z, dot);
+      dot = fmaf(a.w, g.w, dot);
+      d4[r] = make_float4(T * a.x * (g.x - dot), T * a.y * (g.y - dot), T * a.z * (g.z - dot),
+                          T * a.w * (g.w - dot));
+    }
+    return;
+  }
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += stride) {
     const float* sr = s + r * Q;
     const float* gr = ds + r * Q;
     float dot = 0.0f;
@@ -249,6 +276,85 @@ __global__ __launch_bounds__(kWave) void gram_kernel(const float* __restrict__ X
       }
 }
 
+// v2 Gram: k step 16 per fragment, the next step's fragments requested
+// before this step's MFMAs (ping-pong registers, loop unrolled by two so
+// nothing is copied).  Lane (r, h) loads X[row][kb + 8h .. kb + 8h + 8)
+// (two float4); MFMA t covers k = kb + t (h = 0) and kb + 8 + t (h = 1).
+// Loads are unconditional (clamped row, zero select) so every path issues
+// the same VMEM ops.  Needs K % 16 == 0 and kslice % 32 == 0.
+struct Frag8 {
+  float v[2][8];
+};
+__device__ __forceinline__ void load_rows8(const float* __restrict__ base, int row0, int nrows,
+                                           int K, int k0, float (&o)[2][8]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = row0 + u * 32;
+    const bool ok = row < nrows;
+    const float4* p = reinterpret_cast<const float4*>(base + (size_t)(ok ? row : 0) * K + k0);
+    const float4 a = p[0], b = p[1];
+    o[u][0] = ok ? a.x : 0.0f; o[u][1] = ok ? a.y : 0.0f; o[u][2] = ok ? a.z : 0.0f;
+    o[u][3] = ok ? a.w : 0.0f; o[u][4] = ok ? b.x : 0.0f; o[u][5] = ok ? b.y : 0.0f;
+    o[u][6] = ok ? b.z : 0.0f; o[u][7] = ok ? b.w : 0.0f;
+  }
+}
+
+__global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ X,
+                                                     const float* __restrict__ Y, int N, int K,
+                                                     int ntile, int npairs, int symmetric,
+                                                     int ksplit, int kslice,
+                                                     float* __restrict__ part) {
+  const int b = blockIdx.x;
+  const int xcd = b & 7, m = b >> 3;
+  const int split = (m / npairs) * 8 + xcd;
+  const int pair = m % npairs;
+  if (split >= ksplit) return;
+  int ti, tj;
+  pair_tiles(pair, ntile, symmetric, &ti, &tj);
+  const int lane = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const int k_lo = split * kslice, k_hi = min(K, k_lo + kslice);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[u][v] = (f32x16){};
+  const int xr = ti * 64 + r, yr = tj * 64 + r;
+  auto fetch = [&](int kb, float (&xa)[2][8], float (&yb)[2][8]) {
+    const int k0 = min(kb, K - 16) + 8 * h;  // past k_hi: a valid address, product masked below
+    load_rows8(X, xr, N, K, k0, xa);
+    load_rows8(Y, yr, N, K, k0, yb);
+  };
+  auto compute = [&](int kb, float (&xa)[2][8], float (&yb)[2][8]) {
+    if (kb >= k_hi) return;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[u][t], yb[v][t], acc[u][v], 0, 0, 0);
+  };
+  float xa0[2][8], yb0[2][8], xa1[2][8], yb1[2][8];
+  fetch(k_lo, xa0, yb0);
+  for (int kb = k_lo; kb < k_hi; kb += 32) {
+    fetch(kb + 16, xa1, yb1);
+    compute(kb, xa0, yb0);
+    fetch(kb + 32, xa0, yb0);
+    compute(kb + 16, xa1, yb1);
+  }
+  float* out = part + ((size_t)split * npairs + pair) * 64 * 64;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+        out[(u * 32 + row) * 64 + v * 32 + r] = acc[u][v][q];
+      }
+}
+
 // G[i][j] = sum over splits (fixed order, fp64); symmetric tiles mirrored
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ part, int N,
                                                          int ntile, int npairs, int ksplit,
@@ -374,6 +480,84 @@ __global__ __launch_bounds__(kWave) void mf_kernel(const float* __restrict__ Mm,
         const int row = rt * 64 + u * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
         const int col = c0 + v * 32 + r;
         if (row < N && col < K) out[(size_t)row * K + col] = acc[u][v][q];
+      }
+}
+
+// v2 dF = M F: 16 n per step, next step's operands requested before this
+// step's 32 MFMAs (ping-pong registers, unrolled by two).  Lane (r, h)
+// supplies M[row][nb + 8h + t] and F[nb + 8h + t][col]; rows / n / cols past
+// the edges read a clamped address and contribute 0 (M entry zeroed).
+__global__ __launch_bounds__(kWave) void mf_kernel2(const float* __restrict__ Mm,
+                                                   const float* __restrict__ F, int N, int K,
+                                                   int row0, int nrows, int nrowt, int ncolb,
+                                                   float* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int xcd = b & 7, m = b >> 3;
+  const int rt = m % nrowt;
+  const int cb = (m / nrowt) * 8 + xcd;
+  if (cb >= ncolb) return;
+  const int lane = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const int c0 = cb * 64;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[u][v] = (f32x16){};
+  // buffer (SRD) loads: lane part of the offset in voffset, the uniform n
+  // part in soffset; rows of F past N and rows of M past N read out of
+  // bounds (0); n past N within an M row is masked
+  const rsrc_t rm = make_rsrc(Mm, (uint32_t)((size_t)N * N * 4));
+  const rsrc_t rf = make_rsrc(F, (uint32_t)((size_t)N * K * 4));
+  int mvo[2], fvo[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = rt * 64 + u * 32 + r;  // output row; M row row0 + row
+    mvo[u] = row < nrows ? ((row0 + row) * N + 8 * h) * 4 : 0x7FFFFFF0;
+    const int col = c0 + u * 32 + r;
+    fvo[u] = ((8 * h) * K + (col < K ? col : K - 1)) * 4;
+  }
+  auto fetch = [&](int nb, float (&ma)[2][8], float (&fb)[2][8]) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const bool nok = nb + 8 * h + t < N;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float mv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rm, mvo[u], (nb + t) * 4, 0));
+        ma[u][t] = nok ? mv : 0.0f;
+      }
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        fb[v][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rf, fvo[v], (nb + t) * K * 4, 0));
+    }
+  };
+  auto compute = [&](int nb, float (&ma)[2][8], float (&fb)[2][8]) {
+    if (nb >= N) return;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(ma[u][t], fb[v][t], acc[u][v], 0, 0, 0);
+  };
+  float ma0[2][8], fb0[2][8], ma1[2][8], fb1[2][8];
+  fetch(0, ma0, fb0);
+  for (int nb = 0; nb < N; nb += 32) {
+    fetch(nb + 16, ma1, fb1);
+    compute(nb, ma0, fb0);
+    fetch(nb + 32, ma0, fb0);
+    compute(nb + 16, ma1, fb1);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = rt * 64 + u * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const int col = c0 + v * 32 + r;
+        if (row < nrows && col < K) out[(size_t)row * K + col] = acc[u][v][q];
       }
 }
 
@@ -667,8 +851,12 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
   const GramPlan g = gram_plan(N, K, symmetric != 0);
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
-  hipLaunchKernelGGL(gram_kernel, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
-                     g.npairs, symmetric, g.ksplit, g.kslice, part);
+  if (K % 16 == 0)
+    hipLaunchKernelGGL(gram_kernel2, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
+                       g.npairs, symmetric, g.ksplit, g.kslice, part);
+  else
+    hipLaunchKernelGGL(gram_kernel, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
+                       g.npairs, symmetric, g.ksplit, g.kslice, part);
   const size_t total = (size_t)g.npairs * 4096;
   hipLaunchKernelGGL(gram_reduce_kernel, dim3(grid_for((int64_t)total)), dim3(256), 0, st, part, N,
                      g.ntile, g.npairs, g.ksplit, symmetric, G);
@@ -700,7 +888,7 @@ extern "C" int trex_tree_surrogate(const float* S, const float* A, int N, int64_
     const int nrowt = (N + 63) / 64;
     const int ncolb = (int)((K + 63) / 64);
     const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
-    hipLaunchKernelGGL(mf_kernel, dim3(blocks), dim3(kWave), 0, st, M, S, N, (int)K, nrowt, ncolb,
+    hipLaunchKernelGGL(mf_kernel2, dim3(blocks), dim3(kWave), 0, st, M, S, N, (int)K, 0, N, nrowt, ncolb,
                        dS);
   }
   if (G_out &&
@@ -823,14 +1011,22 @@ extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N
   return tree_hip_check("trex_tree_surrogate_combine");
 }
 
-extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,
-                            void* stream) {
-  if (!M || !S || !dS || N <= 0 || K <= 0 || K > 0x7FFFFFFF)
-    return set_error(TREX_E_ARG, "trex_tree_mf: bad arguments");
-  const int nrowt = (N + 63) / 64;
+extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t K, int row0,
+                                 int nrows, float* dS_rows, void* stream) {
+  if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
+      row0 + nrows > N)
+    return set_error(TREX_E_ARG, "trex_tree_mf_rows: bad arguments");
+  if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
+    return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows: S exceeds 2 GiB");
+  const int nrowt = (nrows + 63) / 64;
   const int ncolb = (int)((K + 63) / 64);
   const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
-  hipLaunchKernelGGL(mf_kernel, dim3(blocks), dim3(kWave), 0, (hipStream_t)stream, M, S, N,
-                     (int)K, nrowt, ncolb, dS);
-  return tree_hip_check("trex_tree_mf");
+  hipLaunchKernelGGL(mf_kernel2, dim3(blocks), dim3(kWave), 0, (hipStream_t)stream, M, S, N,
+                     (int)K, row0, nrows, nrowt, ncolb, dS_rows);
+  return tree_hip_check("trex_tree_mf_rows");
+}
+
+extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,
+                            void* stream) {
+  return trex_tree_mf_rows(M, S, N, K, 0, N, dS, stream);
 }

@@ -343,7 +343,9 @@ class TreeOptimizer:
                                              ptr(self.dA), ptr(self.M), ptr(self.ws), st))
         check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
                                       ptr(self.dA), ptr(self.ws), st))
-        check(L_.trex_tree_mf(ptr(self.M), ptr(self.S), N, K, ptr(self.dS), st))
+        # d loss / dS for the ancestor rows only (leaf rows are fixed data)
+        check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
+                                   ptr(self.dS[self.n_leaf:]), st))
         check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc, 1.0,
                                            ptr(self.grads["tree_params"]), st))
         check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]), ptr(self.dS[self.n_leaf:]),
