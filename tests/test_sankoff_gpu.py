@@ -359,3 +359,50 @@ def test_repeated_launches_reset_reduction_counters(device):
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(out["tree_score"], t0) and torch.equal(out["d_cost"], dd0)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json configs as parity cases
+# ---------------------------------------------------------------------------
+def test_config_c1_balanced_8x100x4_hard_forward(device):
+    """C1 (BASELINE configs[0]): balanced 8-leaf tree numbered as
+    src/trex/evals/benchmark.py:781-791 (parents [8,8,9,9,...,14,14]),
+    C = 1 - I, leaves uniform in [0,4) from numpy PCG64(seed=0), integer-cost
+    forward + trex backtrack: bit-exact vs the restatement."""
+    from trex_amd.topology import create_balanced_binary_tree
+
+    adj = create_balanced_binary_tree(8)
+    assert list(adj[:14].argmax(1)) == [8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14]
+    seqs = np.random.Generator(np.random.PCG64(0)).integers(0, 4, size=(8, 100)).astype(np.float32)
+    cost = hamming(4)
+    recon, dp, total = run_sankoff(adj, cost, seqs, 15, 4, 8, return_path=True, device=device)
+    r_recon, r_dp, r_total = run_sankoff_ref(adj, cost, seqs, 15, 4, 8, return_path=True)
+    np.testing.assert_array_equal(dp.cpu().numpy(), r_dp)
+    np.testing.assert_array_equal(recon.cpu().numpy(), r_recon)
+    assert float(total) == float(r_total)
+
+
+@pytest.mark.parametrize("tau", [1.0, 0.1])
+@pytest.mark.parametrize("sim", [True, False])
+def test_config_c2_full_size_softmin_fwd_grad(device, tau, sim):
+    """C2 (BASELINE configs[1]) at full size: balanced 64-taxa tree x 10 000
+    sites x 4 states, C = 1 - I, leaves simulated along the tree (restated
+    ground_truth.mutate, 5 mutations per edge, seed 1) or iid uniform (seed 2);
+    score and d score / d C vs the fp64 oracle at rtol 1e-5."""
+    from trex_amd.topology import children_from_adjacency, create_balanced_binary_tree
+
+    nl, L, Q = 64, 10000, 4
+    if sim:
+        seqs, adj = simulate_leaves(nl, L, Q, 5, seed=1)
+        leaves = seqs[None, :nl].astype(np.int8)
+    else:
+        adj = create_balanced_binary_tree(nl)
+        leaves = random_leaves(1, nl, L, Q, seed=2)
+    ch = children_from_adjacency(adj)
+    cost = hamming(Q)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
+    eng = _engine(ch, L, Q, device)
+    fwd, dc, _, _ = eng.fwd_bwd(_dev(leaves, device), _dev(cost, device, torch.float32), tau)
+    np.testing.assert_allclose(fwd.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
+    np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL,
+                               atol=SOFT_RTOL * np.abs(ref["d_cost"]).max())
