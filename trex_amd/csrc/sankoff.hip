@@ -565,14 +565,6 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   __syncthreads();  // the table is written by lanes < Q, read by all
 
   do {
-    // per-item values must not be hoisted out of this (short) loop: the
-    // laundered lane id and LDS bases keep LICM from pinning registers
-    int lane = threadIdx.x;
-    asm volatile("" : "+v"(lane));
-    float* tab = lds;
-    asm volatile("" : "+s"(tab));
-    float* slots = tab + kTabFloats;
-    int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT);
     const int tree = item / A.tiles;
     const int tile = item - tree * A.tiles;
     const int site = (tile * kWave + lane) * SPT;
