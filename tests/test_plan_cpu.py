@@ -58,6 +58,7 @@ def _interpret(plan: TreePlan, b, leaves, cost):
     dp = np.full((plan.n_int, L, Q), np.nan)
     lD = leaf_dp(leaves, Q)
     last = None
+    prev, prev_row = None, -1
     for row_desc, da, db, flags in steps:
         row = row_desc & 0xFFFF
         oslot = (row_desc >> 16) & 0xFF
@@ -66,6 +67,9 @@ def _interpret(plan: TreePlan, b, leaves, cost):
             kind = (d >> 24) & 3
             if kind == 1:
                 D = lD[d & 0xFFFF]
+            elif kind == 2 and d & (1 << 27):  # register bypass: previous step's output
+                assert prev_row == d & 0xFFFF, "bypass child is not the previous step"
+                D = prev
             elif kind == 2:
                 s = (d >> 16) & 0xFF
                 D = slots[s]
@@ -74,8 +78,9 @@ def _interpret(plan: TreePlan, b, leaves, cost):
                 D = np.full((L, Q), SENTINEL)
             acc = acc + (cost[None] + D[:, None, :]).min(axis=2)
         dp[row] = acc
-        if oslot != 0xFF:
+        if oslot != 0xFF and not flags & 4:
             slots[oslot] = acc
+        prev, prev_row = acc, row
         last = row
     assert last == plan.n_int - 1, "root must be the last step"
     return dp
@@ -102,15 +107,18 @@ def test_plan_program_reproduces_oracle(kind):
 
 
 def test_plan_slot_counts_are_sethi_ullman():
-    for n, want in [(8, 3), (64, 6), (256, 8)]:
+    """Sethi-Ullman depth minus the register bypass: the child evaluated
+    right before its parent never takes a slot, so a balanced tree of n
+    leaves needs log2(n) slots (not log2(n) + 1) and a caterpillar none."""
+    for n, want in [(8, 2), (64, 5), (256, 7)]:
         assert TreePlan.from_adjacency(create_balanced_binary_tree(n)).n_slots == want
-    # a caterpillar needs a single slot
+    # a caterpillar: every internal child is the previous step
     n = 20
     ch = np.full((1, 2 * n - 1, 2), -1, np.int32)
     ch[0, n] = (0, 1)
     for k in range(1, n - 1):
         ch[0, n + k] = (k + 1, n + k - 1)
-    assert TreePlan(ch).n_slots == 1
+    assert TreePlan(ch).n_slots == 0
 
 
 def test_plan_rejects_bad_children():

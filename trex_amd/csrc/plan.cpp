@@ -112,17 +112,29 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
   visit(ni - 1);
   if ((int)order.size() != ni) return false;  // unreachable in a DAG of lower ids
 
-  // slot simulation
+  // register bypass: in this post-order the step right before a node is its
+  // last-evaluated child; when that child has no other consumer its vector
+  // never needs a slot (forward D, adjoint cotangent stay in registers)
+  std::vector<int> pos(ni, 0), consumer(ni, -1);
+  for (int k = 0; k < ni; ++k) pos[order[k]] = k;
+  for (int r = 0; r < ni; ++r)
+    for (int k = 0; k < 2; ++k)
+      if (kids[2 * r + k].kind == kKindInt) consumer[kids[2 * r + k].index] = r;
+  std::vector<char> bypass(ni, 0);
+  for (int r = 0; r < ni; ++r)
+    bypass[r] = refs[r] == 1 && consumer[r] >= 0 && pos[consumer[r]] == pos[r] + 1;
+
+  // slot simulation (bypassed vectors take no slot)
   std::vector<int> remaining(refs), slot(ni, 0xFF);
   std::set<int> free_slots;
   int top = 0, maxs = 0;
   for (int r : order) {
     for (int k = 0; k < 2; ++k) {
       const Child& cd = kids[2 * r + k];
-      if (cd.kind != kKindInt) continue;
+      if (cd.kind != kKindInt || bypass[cd.index]) continue;
       if (--remaining[cd.index] == 0) free_slots.insert(slot[cd.index]);
     }
-    if (refs[r] > 0) {
+    if (refs[r] > 0 && !bypass[r]) {
       int s;
       if (!free_slots.empty()) {
         s = *free_slots.begin();
@@ -161,6 +173,7 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
       int32_t d = (cd.index & 0xFFFF) | (cd.kind << 24);
       if (cd.kind == kKindInt) {
         d |= (slot[cd.index] & 0xFF) << 16;
+        if (bypass[cd.index]) d |= kChildPrev;
         if (reach[r]) {
           if (seen[cd.index]) d |= kStepAccumulate;
           seen[cd.index] = 1;
@@ -171,6 +184,7 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
     int32_t f = 0;
     if (r == ni - 1) f |= kStepRoot;
     if (!reach[r]) f |= kStepUnreached;
+    if (bypass[r]) f |= kStepToNext;
     e[3] = f;
   }
   if (order.back() != ni - 1) return false;

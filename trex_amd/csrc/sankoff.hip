@@ -605,6 +605,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 
     float dv[Q][SPT];
     if constexpr (FWD) {
+      float prev[Q][SPT];  // previous step's D (register bypass, kChildPrev)
       I4 nxt = load_step(prog, 0);
       for (int k = 0; k < A.n_int; ++k) {
         const I4 stp = nxt;
@@ -615,7 +616,12 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         for (int c = 0; c < 2; ++c) {
           const int desc = c == 0 ? stp.y : stp.z;
           const int kind = (desc >> 24) & 3;
-          if (kind == kKindInt) {
+          if (desc & kChildPrev) {
+#pragma unroll
+            for (int j = 0; j < Q; ++j)
+#pragma unroll
+              for (int s = 0; s < SPT; ++s) d[c][j][s] = prev[j][s];
+          } else if (kind == kKindInt) {
             lds_get<Q, SPT>(slots, (desc >> 16) & 0xFF, lane, d[c]);
           } else {
             int code[SPT];
@@ -662,7 +668,11 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         const int oslot = (stp.x >> 16) & 0xFF;
 #pragma unroll
         for (int i = 0; i < Q; ++i) bst<SPT>(rdp, voff, (row * Q + i) * rowbytes, dv[i]);
-        if (oslot != 0xFF) lds_put<Q, SPT>(slots, oslot, lane, dv);
+        if (!(stp.w & kStepToNext) && oslot != 0xFF) lds_put<Q, SPT>(slots, oslot, lane, dv);
+#pragma unroll
+        for (int i = 0; i < Q; ++i)
+#pragma unroll
+          for (int s = 0; s < SPT; ++s) prev[i][s] = dv[i][s];
       }
     } else {
       // adjoint only: the root row comes from the table
@@ -722,11 +732,19 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           for (int j = 0; j < Q; ++j) bld<SPT>(rdp, vo, (crow * Q + j) * rowbytes, nd[c][j]);
         }
       };
+      float gnext[Q][SPT];  // cotangent handed to the next reverse step (bypass)
       auto bstep = [&](const I4& stp, float (&cd)[2][Q][SPT]) {
         if (stp.w & kStepUnreached) return;
         const int row = stp.x & 0xFFFF;
         float g[Q][SPT];
-        lds_get<Q, SPT>(slots, (stp.w & kStepRoot) ? kRootSlot : ((stp.x >> 16) & 0xFF), lane, g);
+        if (stp.w & kStepToNext) {
+#pragma unroll
+          for (int i = 0; i < Q; ++i)
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) g[i][s] = gnext[i][s];
+        } else {
+          lds_get<Q, SPT>(slots, (stp.w & kStepRoot) ? kRootSlot : ((stp.x >> 16) & 0xFF), lane, g);
+        }
         if (want_marg) {
 #pragma unroll
           for (int i = 0; i < Q; ++i) bst<SPT>(rmg, voff, (row * Q + i) * rowbytes, g[i]);
@@ -789,7 +807,12 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           } else {
             float gc[Q][SPT];
             message_adjoint<Q, SPT, MODE>(cf, a, cd[c], g, acc, gc);
-            if (kind == kKindInt) {
+            if (desc & kChildPrev) {
+#pragma unroll
+              for (int j = 0; j < Q; ++j)
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) gnext[j][s] = gc[j][s];
+            } else if (kind == kKindInt) {
               const int cslot = (desc >> 16) & 0xFF;
               if (desc & kStepAccumulate) {
                 float old[Q][SPT];

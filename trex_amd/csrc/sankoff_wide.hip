@@ -272,6 +272,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
 
   float dv = 0.0f;
   if constexpr (FWD) {
+    float prev = 0.0f;  // previous step's D (register bypass, kChildPrev)
     I4 nxt = load_step(prog, 0);
     for (int k = 0; k < A.n_int; ++k) {
       const I4 stp = nxt;
@@ -289,7 +290,8 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
             m = wmsg<G, MODE>(cf, X, w, a, bcoef, code == w.i ? 0.0f : kSentinel);
           }
         } else if (kind == kKindInt) {
-          m = wmsg<G, MODE>(cf, X, w, a, bcoef, slots[((desc >> 16) & 0xFF) * kWave + lane]);
+          const float D = (desc & kChildPrev) ? prev : slots[((desc >> 16) & 0xFF) * kWave + lane];
+          m = wmsg<G, MODE>(cf, X, w, a, bcoef, D);
         } else {
           m = tab[Q * G + w.i];
         }
@@ -298,7 +300,8 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
       const int row = stp.x & 0xFFFF;
       const int oslot = (stp.x >> 16) & 0xFF;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dv), rdp, voff, row * rowbytes, 0);
-      if (oslot != 0xFF) slots[oslot * kWave + lane] = dv;
+      if (!(stp.w & kStepToNext) && oslot != 0xFF) slots[oslot * kWave + lane] = dv;
+      prev = dv;
     }
   } else {
     dv = __uint_as_float(
@@ -362,6 +365,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
       }
     };
     prefetch(nstp);
+    float gnext = 0.0f;  // cotangent handed to the next reverse step (bypass)
     for (int k = A.n_int - 1; k >= 0; --k) {
       const I4 stp = nstp;
       const float cd0 = nd[0], cd1 = nd[1];
@@ -371,7 +375,9 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
       }
       if (stp.w & kStepUnreached) continue;
       const int row = stp.x & 0xFFFF;
-      const float g = slots[((stp.w & kStepRoot) ? A.n_slots : ((stp.x >> 16) & 0xFF)) * kWave + lane];
+      const float g = (stp.w & kStepToNext)
+                          ? gnext
+                          : slots[((stp.w & kStepRoot) ? A.n_slots : ((stp.x >> 16) & 0xFF)) * kWave + lane];
       if (want_marg)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), rmg, voff, row * rowbytes, 0);
       if (want_anc) {
@@ -404,9 +410,13 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
           }
         } else if (kind == kKindInt) {
           float gc = wadj<G, MODE>(cf, X, w, a, c == 0 ? cd0 : cd1, g, acc);
-          const int cslot = (desc >> 16) & 0xFF;
-          if (desc & kStepAccumulate) gc += slots[cslot * kWave + lane];
-          slots[cslot * kWave + lane] = gc;
+          if (desc & kChildPrev) {
+            gnext = gc;
+          } else {
+            const int cslot = (desc >> 16) & 0xFF;
+            if (desc & kStepAccumulate) gc += slots[cslot * kWave + lane];
+            slots[cslot * kWave + lane] = gc;
+          }
         } else {
           (void)wadj<G, MODE>(cf, X, w, a, kSentinel, g, acc);
         }

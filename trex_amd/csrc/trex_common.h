@@ -14,9 +14,14 @@ constexpr int32_t kPlanMagic = 0x54524558;  // 'TREX'
 
 // forward-step child descriptor: index bits 0-15, slot 16-23, kind 24-25
 constexpr int32_t kStepAccumulate = 1 << 26;  // adjoint: add into the slot
+// register bypass: this internal child is the previous step's node (its only
+// consumer is this step): forward reads its D from registers, the adjoint
+// hands its cotangent to the next reverse step in registers
+constexpr int32_t kChildPrev = 1 << 27;
 // forward-step flags (word 3)
 constexpr int32_t kStepRoot = 1;
 constexpr int32_t kStepUnreached = 2;
+constexpr int32_t kStepToNext = 4;  // output consumed only by the next step (bypass)
 
 // backtrack entry kinds (bits 16-19 of word 0)
 constexpr int kBtRoot = 0;
