@@ -76,5 +76,40 @@ __device__ __forceinline__ double wave_sum_strided(const double* p, int n, int l
   return wave_sum(v);
 }
 
+// packed FP32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes of work per VALU op)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk(float x, float y) { return f2{x, y}; }
+__device__ __forceinline__ void pfma(float& d0, float& d1, f2 a, f2 b) {
+  const f2 r = __builtin_elementwise_fma(a, b, f2{d0, d1});
+  d0 = r.x;
+  d1 = r.y;
+}
+// s = sum_j k[j] u[j] (pairs of j per packed op)
+template <int Q>
+__device__ __forceinline__ float kdot(const float (&krow)[Q], const float (&u)[Q]) {
+  if constexpr (Q % 2 == 0) {
+    f2 acc = pk(krow[0], krow[1]) * pk(u[0], u[1]);
+#pragma unroll
+    for (int j = 2; j < Q; j += 2) acc = __builtin_elementwise_fma(pk(krow[j], krow[j + 1]), pk(u[j], u[j + 1]), acc);
+    return acc.x + acc.y;
+  } else {
+    float acc = krow[0] * u[0];
+#pragma unroll
+    for (int j = 1; j < Q; ++j) acc = fmaf(krow[j], u[j], acc);
+    return acc;
+  }
+}
+// acc[j] += r * v[j]
+template <int Q>
+__device__ __forceinline__ void axpy(float (&acc)[Q], float r, const float (&v)[Q]) {
+  if constexpr (Q % 2 == 0) {
+#pragma unroll
+    for (int j = 0; j < Q; j += 2) pfma(acc[j], acc[j + 1], pk(r, r), pk(v[j], v[j + 1]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < Q; ++j) acc[j] = fmaf(r, v[j], acc[j]);
+  }
+}
+
 }  // namespace
 }  // namespace trex

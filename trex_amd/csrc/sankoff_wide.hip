@@ -116,10 +116,7 @@ __device__ __forceinline__ float wmsg(const WCoef<G>& cf, float* X, const WLane&
     const float u = w.pad ? 0.0f : fast_exp2((md - D) * a);
     float uu[G];
     xchg<G>(X + kWave, w.lane, w.gbase, u, uu);
-    float s = cf.row[0] * uu[0];
-#pragma unroll
-    for (int j = 1; j < G; ++j) s = fmaf(cf.row[j], uu[j], s);
-    return fmaf(-bcoef, fast_log2(s), md + cf.cmin);
+    return fmaf(-bcoef, fast_log2(kdot<G>(cf.row, uu)), md + cf.cmin);
   } else {
     float x[G];
     float mn = INFINITY;
@@ -151,17 +148,10 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
     const float u = w.pad ? 0.0f : fast_exp2((md - D) * a);
     float uu[G];
     xchg<G>(X + kWave, w.lane, w.gbase, u, uu);
-    float s = cf.row[0] * uu[0];
-#pragma unroll
-    for (int j = 1; j < G; ++j) s = fmaf(cf.row[j], uu[j], s);
-    const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(s);
-#pragma unroll
-    for (int j = 0; j < G; ++j) acc[j] = fmaf(r, uu[j], acc[j]);
+    const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(kdot<G>(cf.row, uu));
+    axpy<G>(acc, r, uu);
     xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
-    float t = rr[0] * cf.col[0];
-#pragma unroll
-    for (int j = 1; j < G; ++j) t = fmaf(rr[j], cf.col[j], t);
-    return u * t;
+    return u * kdot<G>(cf.col, rr);
   } else if constexpr (MODE == kHard) {
     float x[G];
     float mn = cf.row[0] + d[0];
@@ -201,8 +191,7 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
       s += e[j];
     }
     const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(s);
-#pragma unroll
-    for (int j = 0; j < G; ++j) acc[j] += r * e[j];
+    axpy<G>(acc, r, e);
     float mm[G];
     xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
     xchg<G>(X + 3 * kWave, w.lane, w.gbase, w.pad ? 0.0f : mn, mm);
