@@ -194,6 +194,12 @@ int trex_tree_surrogate(const float* S, const float* A, int N, int64_t K, float*
  * diag(r+c) - (A+A^T) from (A, G);  dS = M S.  Workspace for combine: >= 8*N B. */
 int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
                    int64_t workspace_bytes, void* stream);
+/* As trex_tree_gram, but leaves G[i][j] untouched where both i and j lie in
+ * the first floor(skip_rows/64)*64 rows: a cached constant block, e.g. the
+ * fixed leaf x leaf Gram of the optimisation loop (leaf rows of S are data,
+ * tree.py:127 rewrites only the ancestor rows). */
+int trex_tree_gram_skip(const float* S, int N, int64_t K, int skip_rows, float* G,
+                        void* workspace, int64_t workspace_bytes, void* stream);
 int trex_tree_surrogate_combine(const float* A, const float* G, int N, float* loss, float* dA,
                                 float* M, void* workspace, void* stream);
 int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS, void* stream);

@@ -225,3 +225,25 @@ def test_mf_rows_equals_full_dS_slice(device, N, K, row0):
     assert torch.equal(part, full[row0:])
     ref = _n(M).astype(np.float64) @ _n(S)
     np.testing.assert_allclose(_n(full), ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+
+
+def test_gram_skip_keeps_cached_block(device):
+    """trex_tree_gram_skip recomputes every tile except the leading constant
+    block, which keeps its previous contents (the optimiser's cached
+    leaf x leaf Gram); the other entries equal the full Gram bitwise."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    rng = np.random.default_rng(3)
+    N, K, skip = 300, 1024, 130  # tiles 0-1 (rows < 128) skipped
+    S = _t(rng.random((N, K)), device)
+    ws = torch.empty(int(lib().trex_tree_workspace_bytes(N, K)), dtype=torch.uint8, device=device)
+    st = stream_handle(torch.device(device))
+    full = torch.empty((N, N), device=device)
+    check(lib().trex_tree_gram(ptr(S), N, K, ptr(full), ptr(ws), ws.numel(), st))
+    G = torch.full((N, N), -7.0, device=device)
+    check(lib().trex_tree_gram_skip(ptr(S), N, K, skip, ptr(G), ptr(ws), ws.numel(), st))
+    t0 = (skip // 64) * 64
+    assert torch.all(G[:t0, :t0] == -7.0)
+    mask = torch.ones((N, N), dtype=torch.bool, device=device)
+    mask[:t0, :t0] = False
+    assert torch.equal(G[mask], full[mask])

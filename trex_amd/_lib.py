@@ -54,6 +54,7 @@ SIGNATURES = {
     "trex_tree_workspace_bytes": (_c_i64, [_c_i, _c_i64]),
     "trex_tree_surrogate": (_c_i, [_p, _p, _c_i, _c_i64, _p, _p, _p, _p, _p, _c_i64, _p]),
     "trex_tree_gram": (_c_i, [_p, _c_i, _c_i64, _p, _p, _c_i64, _p]),
+    "trex_tree_gram_skip": (_c_i, [_p, _c_i, _c_i64, _c_i, _p, _p, _c_i64, _p]),
     "trex_tree_surrogate_combine": (_c_i, [_p, _p, _c_i, _p, _p, _p, _p, _p]),
     "trex_tree_mf": (_c_i, [_p, _p, _c_i, _c_i64, _p, _p]),
     "trex_tree_mf_rows": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _p, _p]),

@@ -217,12 +217,19 @@ __device__ __forceinline__ void load_frag16(const float* __restrict__ base, int 
   }
 }
 
-__device__ __forceinline__ void pair_tiles(int pair, int ntile, int symmetric, int* ti, int* tj) {
-  if (symmetric) {  // (ti <= tj), row-major over the upper triangle
+// pair -> (ti, tj).  symmetric: the upper triangle (ti <= tj) row-major,
+// minus the tiles with both ti, tj < t0 (a cached constant block, e.g. the
+// fixed leaf x leaf Gram of the C5 loop)
+__host__ __device__ __forceinline__ int sym_row_len(int a, int ntile, int t0) {
+  return ntile - (a > t0 ? a : t0);
+}
+__device__ __forceinline__ void pair_tiles(int pair, int ntile, int symmetric, int t0, int* ti,
+                                           int* tj) {
+  if (symmetric) {
     int a = 0, rem = pair;
-    while (rem >= ntile - a) { rem -= ntile - a; ++a; }
+    while (rem >= sym_row_len(a, ntile, t0)) { rem -= sym_row_len(a, ntile, t0); ++a; }
     *ti = a;
-    *tj = a + rem;
+    *tj = (a > t0 ? a : t0) + rem;
   } else {
     *ti = pair / ntile;
     *tj = pair % ntile;
@@ -231,7 +238,7 @@ __device__ __forceinline__ void pair_tiles(int pair, int ntile, int symmetric, i
 
 __global__ __launch_bounds__(kWave) void gram_kernel(const float* __restrict__ X,
                                                     const float* __restrict__ Y, int N, int K,
-                                                    int ntile, int npairs, int symmetric,
+                                                    int ntile, int npairs, int symmetric, int t0,
                                                     int ksplit, int kslice,
                                                     float* __restrict__ part) {
   const int b = blockIdx.x;
@@ -240,7 +247,7 @@ __global__ __launch_bounds__(kWave) void gram_kernel(const float* __restrict__ X
   const int pair = m % npairs;
   if (split >= ksplit) return;
   int ti, tj;
-  pair_tiles(pair, ntile, symmetric, &ti, &tj);
+  pair_tiles(pair, ntile, symmetric, t0, &ti, &tj);
   const int lane = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
   const int k_lo = split * kslice, k_hi = min(K, k_lo + kslice);
@@ -301,7 +308,7 @@ __device__ __forceinline__ void load_rows8(const float* __restrict__ base, int r
 
 __global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ X,
                                                      const float* __restrict__ Y, int N, int K,
-                                                     int ntile, int npairs, int symmetric,
+                                                     int ntile, int npairs, int symmetric, int t0,
                                                      int ksplit, int kslice,
                                                      float* __restrict__ part) {
   const int b = blockIdx.x;
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ 
   const int pair = m % npairs;
   if (split >= ksplit) return;
   int ti, tj;
-  pair_tiles(pair, ntile, symmetric, &ti, &tj);
+  pair_tiles(pair, ntile, symmetric, t0, &ti, &tj);
   const int lane = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
   const int k_lo = split * kslice, k_hi = min(K, k_lo + kslice);
@@ -358,13 +365,14 @@ __global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ 
 // G[i][j] = sum over splits (fixed order, fp64); symmetric tiles mirrored
 __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restrict__ part, int N,
                                                          int ntile, int npairs, int ksplit,
-                                                         int symmetric, float* __restrict__ G) {
+                                                         int symmetric, int t0,
+                                                         float* __restrict__ G) {
   const size_t total = (size_t)npairs * 4096;
   for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
     const int pair = (int)(t / 4096);
     const int e = (int)(t % 4096);
     int ti, tj;
-    pair_tiles(pair, ntile, symmetric, &ti, &tj);
+    pair_tiles(pair, ntile, symmetric, t0, &ti, &tj);
     double s = 0.0;
     for (int sp = 0; sp < ksplit; ++sp) s += (double)part[((size_t)sp * npairs + pair) * 4096 + e];
     const int i = ti * 64 + e / 64, j = tj * 64 + e % 64;
@@ -809,11 +817,16 @@ namespace {
 struct GramPlan {
   int ntile, npairs, ksplit, kslice;
 };
-GramPlan gram_plan(int N, int64_t K, bool symmetric = false) {
+GramPlan gram_plan(int N, int64_t K, bool symmetric = false, int t0 = 0) {
   GramPlan g;
   g.ntile = (N + 63) / 64;
   // workspace is sized for the full (non-symmetric) tile set
-  g.npairs = symmetric ? g.ntile * (g.ntile + 1) / 2 : g.ntile * g.ntile;
+  if (symmetric) {
+    g.npairs = 0;
+    for (int a = 0; a < g.ntile; ++a) g.npairs += sym_row_len(a, g.ntile, t0);
+  } else {
+    g.npairs = g.ntile * g.ntile;
+  }
   // enough waves to fill 256 CUs several times; slices multiple of 32
   int ks = (int)std::max<int64_t>(1, std::min<int64_t>(256, (4096 + g.npairs - 1) / g.npairs));
   ks = (ks + 7) / 8 * 8;
@@ -847,19 +860,20 @@ extern "C" int64_t trex_tree_workspace_bytes(int N, int64_t K) {
 
 namespace {
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
-         hipStream_t st) {
-  const GramPlan g = gram_plan(N, K, symmetric != 0);
+         hipStream_t st, int t0 = 0) {
+  const GramPlan g = gram_plan(N, K, symmetric != 0, t0);
+  if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
   if (K % 16 == 0)
     hipLaunchKernelGGL(gram_kernel2, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
-                       g.npairs, symmetric, g.ksplit, g.kslice, part);
+                       g.npairs, symmetric, t0, g.ksplit, g.kslice, part);
   else
     hipLaunchKernelGGL(gram_kernel, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
-                       g.npairs, symmetric, g.ksplit, g.kslice, part);
+                       g.npairs, symmetric, t0, g.ksplit, g.kslice, part);
   const size_t total = (size_t)g.npairs * 4096;
   hipLaunchKernelGGL(gram_reduce_kernel, dim3(grid_for((int64_t)total)), dim3(256), 0, st, part, N,
-                     g.ntile, g.npairs, g.ksplit, symmetric, G);
+                     g.ntile, g.npairs, g.ksplit, symmetric, t0, G);
   return tree_hip_check("gram");
 }
 }  // namespace
@@ -990,13 +1004,20 @@ extern "C" int trex_tree_discretize(const float* A, int nrows, int ncols, int n_
 
 // ---- split surrogate phases (for site-sharded multi-GPU: all-reduce G between
 // trex_tree_gram and trex_tree_surrogate_combine) ----
+extern "C" int trex_tree_gram_skip(const float* S, int N, int64_t K, int skip_rows, float* G,
+                                   void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!S || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF || skip_rows < 0 ||
+      skip_rows > N)
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip: bad arguments");
+  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip: workspace too small");
+  return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream,
+              skip_rows / 64);
+}
+
 extern "C" int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
                               int64_t workspace_bytes, void* stream) {
-  if (!S || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF)
-    return set_error(TREX_E_ARG, "trex_tree_gram: bad arguments");
-  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
-    return set_error(TREX_E_ARG, "trex_tree_gram: workspace too small");
-  return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream);
+  return trex_tree_gram_skip(S, N, K, 0, G, workspace, workspace_bytes, stream);
 }
 
 extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N, float* loss,

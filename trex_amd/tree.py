@@ -323,6 +323,14 @@ class TreeOptimizer:
         self.ws = torch.empty(int(lib().trex_tree_workspace_bytes(self.N, self.K)),
                               dtype=torch.uint8, device=dev)
         self.opt = Adam(self.params, lr, clip_norm=clip_norm)
+        # the leaf x leaf block of G = S S^T is constant (leaf rows are data):
+        # computed once here, skipped by every step's Gram.  With site
+        # sharding the Gram is all-reduced in place, so it is recomputed.
+        self.skip_rows = 0
+        if group is None:
+            check(lib().trex_tree_gram(ptr(self.S), self.N, self.K, ptr(self.G), ptr(self.ws),
+                                       self.ws.numel(), stream_handle(dev)))
+            self.skip_rows = self.n_leaf
 
     def step(self, temperature: float, noise):
         """One optimisation step; returns the (device) loss before the update."""
@@ -335,8 +343,8 @@ class TreeOptimizer:
                                       ptr(self.S[self.n_leaf:]), st))
         check(L_.trex_tree_update_tree(ptr(p["tree_params"]), ptr(noise), None, N, self.n_anc,
                                        1.0, ptr(self.A), st))
-        check(L_.trex_tree_gram(ptr(self.S), N, K, ptr(self.G), ptr(self.ws), self.ws.numel(),
-                                st))
+        check(L_.trex_tree_gram_skip(ptr(self.S), N, K, self.skip_rows, ptr(self.G),
+                                     ptr(self.ws), self.ws.numel(), st))
         if self.reducer is not None:
             self.reducer(self.G)
         check(L_.trex_tree_surrogate_combine(ptr(self.A), ptr(self.G), N, ptr(self.loss),
