@@ -83,10 +83,10 @@ int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
  *            sankoff.py:50)
  *   cost     fp32  [Q][Q]            substitution cost C[parent][child]
  *   tau      0 => hard min-plus (trex); >0 => softmin relaxation
- *   dp       fp32  internal rows (required), layout by Q:
- *            Q <= 4: [B][n_int][Q][L]  (sites innermost; lane-per-site kernels)
- *            4 < Q <= 32: [B][n_int][L][Q]  (site-major; lane-per-state
- *            kernels, e.g. protein Q = 20) -- see trex_dp_site_major
+ *   dp       fp32  internal rows (required), site-major [B][n_int][L][Q]
+ *            (the reference's per-site (n_all, Q) rows without the leaf
+ *            rows; a lane's Q states are one 8/12/16-byte access for Q <= 4,
+ *            a lane group's row for the lane-per-state kernels, Q > 4)
  *   site_score fp32 [B][L] or NULL;  tree_score fp32 [B] (required)
  * Q > 32 returns TREX_E_UNSUPPORTED.
  * ---------------------------------------------------------------------- */
@@ -134,7 +134,7 @@ int trex_sankoff_fwd_bwd(const int32_t* plan, int n_slots, const int8_t* leaves,
  * reference's DFS (backtrack_sankoff_jit, sankoff.py:191-267) re-deriving
  * each child's state as the first argmin of C[s_parent] + D_child
  * (sankoff.py:67-69) instead of storing the backtracking table.
- *   dp         fp32 DP table (either layout) from a tau=0 forward
+ *   dp         fp32 DP table from a tau=0 forward
  *   anc_states int8 [B][n_int][L] out (0 for nodes the DFS never reaches)
  * ---------------------------------------------------------------------- */
 int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, const float* cost,
@@ -151,7 +151,8 @@ int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,
                            int n_all, int Q, float* out, void* stream);
 
 /* 1 when the DP / marginal tables for Q states are site-major
- * [B][n_int][L][Q], 0 when they are [B][n_int][Q][L]. */
+ * [B][n_int][L][Q], 0 when they are [B][n_int][Q][L].  Always 1 since
+ * trex_version() 4 (kept so bindings written against v3 still work). */
 int trex_dp_site_major(int Q);
 
 /* ========================================================================

@@ -45,7 +45,7 @@ def test_site_major_layout_flag(device):
     eng = _engine(random_topologies(1, 4, seed=0), 10, 20, device)
     assert eng.site_major and eng.dp_shape == (1, 3, 10, 20)
     eng4 = _engine(random_topologies(1, 4, seed=0), 10, 4, device)
-    assert not eng4.site_major
+    assert eng4.site_major and eng4.dp_shape == (1, 3, 10, 4)  # every Q since v4
 
 
 @pytest.mark.parametrize("Q", [5, 20, 21])

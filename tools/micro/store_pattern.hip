@@ -45,6 +45,23 @@ __global__ __launch_bounds__(64) void tilemajor_kernel(float* dp, int B, int til
   }
 }
 
+// site-major layout [B][n_int][L][Q]: a lane's Q=4 states are one dwordx4
+// store, a wave writes 1 KiB contiguous per node
+__global__ __launch_bounds__(64) void sitemajor_kernel(float* dp, int B, int tiles, int n_int, int L, int grouped) {
+  int b = blockIdx.x;
+  const int nb = B * tiles;
+  if (grouped) { const int per = (nb + 7) / 8; b = (b & 7) * per + (b >> 3); if (b >= nb) return; }
+  const int tree = b / tiles, tile = b % tiles;
+  const int site = tile * 64 + threadIdx.x;
+  if (site >= L) return;
+  float v = (float)threadIdx.x;
+  float4* base = reinterpret_cast<float4*>(dp) + (size_t)tree * n_int * L + site;
+  for (int k = 0; k < n_int; ++k) {
+    base[(size_t)k * L] = make_float4(v, v, v, v);
+    v += 1.0f;
+  }
+}
+
 __global__ void stream_kernel(float4* p, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     p[i] = make_float4(1, 2, 3, 4);
@@ -85,6 +102,11 @@ int main() {
     timeit(nm, [&] { int nb = B * 78; hipLaunchKernelGGL(tilemajor_kernel<1>, dim3((nb + 7) / 8 * 8), dim3(64), 0, 0, dp, B, 78, n_int, Q, g); });
     snprintf(nm, 64, "tilemajor W=4 grouped=%d", g);
     timeit(nm, [&] { int nb = B * 19; hipLaunchKernelGGL(tilemajor_kernel<4>, dim3((nb + 7) / 8 * 8), dim3(64), 0, 0, dp, B, 19, n_int, Q, g); });
+  }
+  for (int g = 0; g < 2; ++g) {
+    char nm[64];
+    snprintf(nm, 64, "sitemajor x4 grouped=%d", g);
+    timeit(nm, [&] { int nb = B * tiles64; hipLaunchKernelGGL(sitemajor_kernel, dim3((nb + 7) / 8 * 8), dim3(64), 0, 0, dp, B, tiles64, n_int, L, g); });
   }
   timeit("stream float4", [&] { hipLaunchKernelGGL(stream_kernel, dim3(8192), dim3(256), 0, 0, (float4*)dp, n / 4); });
   return 0;

@@ -242,6 +242,47 @@ __device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT
   }
 }
 
+// Site-major DP rows ([row][L][Q]): a lane's SPT consecutive sites x Q states
+// are Q*SPT contiguous floats -> one dwordx4 (Q = 4), dwordx3 or dwordx2
+// access per site.  voff = site*Q*4 (per lane), soff = row*L*Q*4.
+template <int Q, int SPT>
+__device__ __forceinline__ void bst_row(rsrc_t r, int voff, int soff, const float (&d)[Q][SPT]) {
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    const int vo = voff + s * Q * 4;
+    if constexpr (Q == 4) {
+      u32x4 w = {__float_as_uint(d[0][s]), __float_as_uint(d[1][s]), __float_as_uint(d[2][s]),
+                 __float_as_uint(d[3][s])};
+      __builtin_amdgcn_raw_buffer_store_b128(w, r, vo, soff, 0);
+    } else if constexpr (Q == 3) {
+      u32x3 w = {__float_as_uint(d[0][s]), __float_as_uint(d[1][s]), __float_as_uint(d[2][s])};
+      __builtin_amdgcn_raw_buffer_store_b96(w, r, vo, soff, 0);
+    } else {
+      u32x2 w = {__float_as_uint(d[0][s]), __float_as_uint(d[1][s])};
+      __builtin_amdgcn_raw_buffer_store_b64(w, r, vo, soff, 0);
+    }
+  }
+}
+
+template <int Q, int SPT>
+__device__ __forceinline__ void bld_row(rsrc_t r, int voff, int soff, float (&d)[Q][SPT]) {
+#pragma unroll
+  for (int s = 0; s < SPT; ++s) {
+    const int vo = voff + s * Q * 4;
+    if constexpr (Q == 4) {
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, 0);
+      d[0][s] = __uint_as_float(w.x); d[1][s] = __uint_as_float(w.y);
+      d[2][s] = __uint_as_float(w.z); d[3][s] = __uint_as_float(w.w);
+    } else if constexpr (Q == 3) {
+      const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(r, vo, soff, 0);
+      d[0][s] = __uint_as_float(w.x); d[1][s] = __uint_as_float(w.y); d[2][s] = __uint_as_float(w.z);
+    } else {
+      const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0);
+      d[0][s] = __uint_as_float(w.x); d[1][s] = __uint_as_float(w.y);
+    }
+  }
+}
+
 // --------------------------------------------------------------------------
 // message M_c[i] = min_j / smin_j (C[i][j] + D_c[j])      (sankoff.py:67-68)
 // --------------------------------------------------------------------------
@@ -432,11 +473,11 @@ struct KArgs {
   int n_int, nl, L, tiles, B, n_slots;
   float a, bcoef;
   int hard_root;
-  float* dp;            // [B][n_int][Q][L] (fwd writes / adjoint reads)
+  float* dp;            // [B][n_int][L][Q] site-major (fwd writes / adjoint reads)
   float* site_score;    // [B][L] or null
   float* tree_score;    // [B]
   const float* dts;     // [B] or null
-  float* marg;          // [B][n_int][Q][L] or null
+  float* marg;          // [B][n_int][L][Q] or null
   int8_t* anc;          // [B][n_int][L] or null
   float* d_cost;        // [Q][Q]
   double* part_tree;    // [B*tiles] per-item score partials
@@ -460,8 +501,14 @@ constexpr int kPrefetchRows = 64;  // leaf tiles of <= 64 leaves are prefetched
 // adjacent tiles (shared L2 lines).  Each item is one (tree, 64*SPT-site
 // tile); the next item's leaf tile is loaded into registers while the
 // current one computes.
-template <int Q, int SPT, int MODE, int PHASE, bool LFAST>
+// RES (fused PHASE 3 only): the LDS-resident variant.  Every internal D
+// vector of the item's tree stays in LDS ([n_int][64][Q], written once by the
+// forward, read by the adjoint), so the adjoint reads nothing from HBM; the
+// Sethi-Ullman slots then hold only cotangents.  Costs n_int*Q*256 B of LDS
+// per wave (31 KiB at 32 taxa: one wave per SIMD).
+template <int Q, int SPT, int MODE, int PHASE, bool LFAST, bool RES>
 __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
+  static_assert(!RES || (PHASE == 3 && SPT == 1), "resident mode is the fused SPT=1 kernel");
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
@@ -482,7 +529,8 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   float* tab = lds;
   float* slots = lds + kTabFloats;
   const int kRootSlot = A.n_slots;
-  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT);
+  float* dres = slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT;  // RES: [n_int][64][Q]
+  int8_t* lleaf = reinterpret_cast<int8_t*>(RES ? dres + (size_t)A.n_int * Q * kWave : dres);
 
   // ---- once per wave: leaf message table T[s][i] = C[i][s], T[Q][i] =
   // message of an all-1e5 row ----
@@ -559,8 +607,8 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
     const uint32_t treebytes = (uint32_t)((size_t)A.n_int * Q * L * 4);
     const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * A.n_int * Q * L, treebytes);
     // inactive lanes address past the buffer: stores drop, loads return 0
-    const int voff = active ? site * 4 : 0x7FFFFFF0;
-    const int rowbytes = L * 4;
+    const int voff = active ? site * Q * 4 : 0x7FFFFFF0;
+    const int rowbytes = L * Q * 4;
 
     auto child_code = [&](int desc, int (&code)[SPT]) {
       ld_codes<SPT>(lleaf + ((desc & 0xFFFF) * kWave + lane) * SPT, code);
@@ -587,7 +635,10 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
               for (int s = 0; s < SPT; ++s) d[c][j][s] = prev[j][s];
           } else if (kind == kKindInt) {
-            lds_get<Q, SPT>(slots, (desc >> 16) & 0xFF, lane, d[c]);
+            if constexpr (RES)
+              lds_get<Q, SPT>(dres, desc & 0xFFFF, lane, d[c]);
+            else
+              lds_get<Q, SPT>(slots, (desc >> 16) & 0xFF, lane, d[c]);
           } else {
             int code[SPT];
             if (kind == kKindLeaf) {
@@ -631,9 +682,12 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         }
         const int row = stp.x & 0xFFFF;
         const int oslot = (stp.x >> 16) & 0xFF;
-#pragma unroll
-        for (int i = 0; i < Q; ++i) bst<SPT>(rdp, voff, (row * Q + i) * rowbytes, dv[i]);
-        if (!(stp.w & kStepToNext) && oslot != 0xFF) lds_put<Q, SPT>(slots, oslot, lane, dv);
+        bst_row<Q, SPT>(rdp, voff, row * rowbytes, dv);
+        if constexpr (RES) {
+          if (!(stp.w & kStepRoot)) lds_put<Q, SPT>(dres, row, lane, dv);
+        } else if (!(stp.w & kStepToNext) && oslot != 0xFF) {
+          lds_put<Q, SPT>(slots, oslot, lane, dv);
+        }
 #pragma unroll
         for (int i = 0; i < Q; ++i)
 #pragma unroll
@@ -641,8 +695,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
       }
     } else {
       // adjoint only: the root row comes from the table
-#pragma unroll
-      for (int i = 0; i < Q; ++i) bld<SPT>(rdp, voff, ((A.n_int - 1) * Q + i) * rowbytes, dv[i]);
+      bld_row<Q, SPT>(rdp, voff, (A.n_int - 1) * rowbytes, dv);
     }
 
     // ---- root: score + cotangent ----
@@ -693,8 +746,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           const bool internal = ((desc >> 24) & 3) == kKindInt;
           const int vo = internal ? voff : 0x7FFFFFF0;
           const int crow = internal ? (desc & 0xFFFF) : 0;
-#pragma unroll
-          for (int j = 0; j < Q; ++j) bld<SPT>(rdp, vo, (crow * Q + j) * rowbytes, nd[c][j]);
+          bld_row<Q, SPT>(rdp, vo, crow * rowbytes, nd[c]);
         }
       };
       float gnext[Q][SPT];  // cotangent handed to the next reverse step (bypass)
@@ -711,8 +763,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           lds_get<Q, SPT>(slots, (stp.w & kStepRoot) ? kRootSlot : ((stp.x >> 16) & 0xFF), lane, g);
         }
         if (want_marg) {
-#pragma unroll
-          for (int i = 0; i < Q; ++i) bst<SPT>(rmg, voff, (row * Q + i) * rowbytes, g[i]);
+          bst_row<Q, SPT>(rmg, voff, row * rowbytes, g);
         }
         if (at && active) {
           int best[SPT];
@@ -792,6 +843,22 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           }
         }
       };
+      if constexpr (RES) {
+        // D of the internal children from the resident table; the next
+        // step's program words are loaded one step ahead
+        I4 sn = load_step(prog, A.n_int - 1);
+        for (int k = A.n_int - 1; k >= 0; --k) {
+          const I4 cur = sn;
+          if (k >= 1) sn = load_step(prog, k - 1);
+          float cd[2][Q][SPT];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int desc = c == 0 ? cur.y : cur.z;
+            if (((desc >> 24) & 3) == kKindInt) lds_get<Q, SPT>(dres, desc & 0xFFFF, lane, cd[c]);
+          }
+          bstep(cur, cd);
+        }
+      } else {
       float bufA[2][Q][SPT], bufB[2][Q][SPT];
       I4 sA = load_step(prog, A.n_int - 1);
       I4 sB = A.n_int > 1 ? load_step(prog, A.n_int - 2) : sA;
@@ -810,6 +877,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         if (k >= 3) sB = load_step(prog, k - 3);
         bstep(cB, bufB);
       }
+      }
 
       // ---- per-item dC partial (fixed-order reduce kernel sums the items) ----
 #pragma unroll
@@ -826,7 +894,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   } while (PERSIST && item < item_end);
 }
 
-template <int Q, int SPT, int MODE, int PHASE>
+template <int Q, int SPT, int MODE, int PHASE, bool RES = false>
 __device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds) {
   // leaf messages have the closed form C[i][code] when the 1e5 sentinel
   // dominates (hard: range(C) < 1e5; soft: exp(-(1e5 - range)/tau) < 2^-64)
@@ -835,9 +903,9 @@ __device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds
   const float range = cmax - cmin;
   const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
   if (lfast)
-    sankoff_body<Q, SPT, MODE, PHASE, true>(A, lds);
+    sankoff_body<Q, SPT, MODE, PHASE, true, RES>(A, lds);
   else
-    sankoff_body<Q, SPT, MODE, PHASE, false>(A, lds);
+    sankoff_body<Q, SPT, MODE, PHASE, false, RES>(A, lds);
 }
 
 template <int Q, int SPT, bool SOFT, int PHASE>
@@ -853,6 +921,24 @@ void sankoff_kernel(KArgs A) {
       sankoff_dispatch_leaf<Q, SPT, kSoftK, PHASE>(A, lds);
     else
       sankoff_dispatch_leaf<Q, SPT, kSoftDirect, PHASE>(A, lds);
+  }
+}
+
+// LDS-resident fused kernel (see sankoff_body, RES): occupancy is set by LDS
+// (one wave per SIMD at 32 taxa), so the register budget is generous
+template <int Q, bool SOFT>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 8)))
+void sankoff_res_kernel(KArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  if constexpr (!SOFT) {
+    sankoff_dispatch_leaf<Q, 1, kHard, 3, true>(A, lds);
+  } else {
+    float cmin, cmax;
+    cost_range<Q>(A.cost, cmin, cmax);
+    if (use_ktrick(cmin, cmax, A.a))
+      sankoff_dispatch_leaf<Q, 1, kSoftK, 3, true>(A, lds);
+    else
+      sankoff_dispatch_leaf<Q, 1, kSoftDirect, 3, true>(A, lds);
   }
 }
 
@@ -874,8 +960,8 @@ __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
 #pragma unroll
     for (int j = 0; j < Q; ++j) c[i][j] = as_const(cost)[i * Q + j];
   const cptr<int> prog = as_const(reinterpret_cast<const int*>(bt)) + (size_t)tree * n_int * 2;
-  const size_t rowstride = (size_t)Q * L;
-  const float* dpt = dp + (size_t)tree * n_int * rowstride + site;
+  const size_t rowstride = (size_t)Q * L;  // site-major rows [L][Q]
+  const float* dpt = dp + (size_t)tree * n_int * rowstride + (size_t)site * Q;
   int8_t* at = anc + (size_t)tree * n_int * L + site;
   for (int k = 0; k < n_int; ++k) {
     const int2 e = make_int2(prog[2 * k], prog[2 * k + 1]);
@@ -890,8 +976,17 @@ __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
       if (kind == kBtSentinel) {
         fill_sentinel<Q, SPT>(d);
       } else {
+        const float* pr = dpt + (size_t)x * rowstride;
 #pragma unroll
-        for (int j = 0; j < Q; ++j) ld<SPT>(dpt + (size_t)x * rowstride + (size_t)j * L, d[j]);
+        for (int t = 0; t < SPT; ++t) {
+          if constexpr (Q == 4) {
+            const float4 v = reinterpret_cast<const float4*>(pr)[t];
+            d[0][t] = v.x; d[1][t] = v.y; d[2][t] = v.z; d[3][t] = v.w;
+          } else {
+#pragma unroll
+            for (int j = 0; j < Q; ++j) d[j][t] = pr[t * Q + j];
+          }
+        }
       }
       if (kind == kBtRoot) {
 #pragma unroll
@@ -931,7 +1026,7 @@ __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
   }
 }
 
-// dp [B][n_int][Q][L] (Q <= 4) / [B][n_int][L][Q] (Q > 4) -> trex VmappedDPTable [B][L][n_all][Q]
+// dp [B][n_int][L][Q] (site-major, every Q) -> trex VmappedDPTable [B][L][n_all][Q]
 __global__ __launch_bounds__(256) void to_trex_layout_kernel(const float* __restrict__ dp,
                                                             const int8_t* __restrict__ leaves,
                                                             int B, int L, int n_all, int nl, int Q,
@@ -949,13 +1044,8 @@ __global__ __launch_bounds__(256) void to_trex_layout_kernel(const float* __rest
       const int code = leaves[((size_t)b * nl + node) * L + l];
       for (int q = 0; q < Q; ++q) o[q] = (code == q) ? 0.0f : kSentinel;
     } else {
-      if (Q > 4) {  // site-major [B][n_int][L][Q]
-        const float* src = dp + (((size_t)b * ni + (node - nl)) * L + l) * Q;
-        for (int q = 0; q < Q; ++q) o[q] = src[q];
-      } else {
-        const float* src = dp + (((size_t)b * ni + (node - nl)) * Q) * L + l;
-        for (int q = 0; q < Q; ++q) o[q] = src[(size_t)q * L];
-      }
+      const float* src = dp + (((size_t)b * ni + (node - nl)) * L + l) * Q;
+      for (int q = 0; q < Q; ++q) o[q] = src[q];
     }
   }
 }
@@ -988,6 +1078,43 @@ size_t lds_bytes(int n_slots, int nl, int Q, int spt) {
   const size_t b = (size_t)kTabFloats * 4 + (size_t)(n_slots + 1) * Q * kWave * spt * 4 +
                    (size_t)nl * kWave * spt;
   return (b + 15) & ~(size_t)15;
+}
+
+// LDS-resident fused kernel: the slot stack (cotangents) plus every internal
+// D vector of the tree
+size_t lds_res_bytes(int n_slots, int nl, int ni, int Q) {
+  const size_t b = (size_t)kTabFloats * 4 + (size_t)(n_slots + 1 + ni) * Q * kWave * 4 +
+                   (size_t)nl * kWave;
+  return (b + 15) & ~(size_t)15;
+}
+constexpr size_t kLdsPerCu = 160 * 1024;
+
+int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return cus;
+}
+
+// Resident mode trades the adjoint's HBM re-read of the DP table for LDS
+// occupancy.  Measured on the C4 shard (32 taxa, 31 KiB per wave, one wave
+// per SIMD) it is 2.3x slower than the re-reading kernel (410 vs 176 us: a
+// lone wave exposes every LDS / scalar-load / transcendental latency), so it
+// is taken only when the grid has at most one wave per CU anyway (C2-like
+// single trees, where it is on par or slightly faster).
+// TREX_RESIDENT=0 / 1 forces it off / on (whenever it fits; tuning).
+bool use_resident(size_t lds_res, int nitems) {
+  static const int forced = [] {
+    const char* e = std::getenv("TREX_RESIDENT");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (lds_res > kLdsPerCu || forced == 0) return false;
+  if (forced == 1) return true;
+  return (long)nitems <= (long)device_cus();
 }
 
 // sites per lane: 1 (measured fastest for the fused soft kernel: SPT=2
@@ -1081,6 +1208,18 @@ void dispatch_q(int phase, int spt, bool soft, size_t lds, hipStream_t st, const
   }
 }
 
+template <int Q>
+void launch_res(bool soft, size_t lds, hipStream_t st, const KArgs& A) {
+  auto go = [&](auto kernel) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kernel, dim3((A.nblocks + 7) / 8 * 8), dim3(kWave), lds, st, A);
+  };
+  if (soft) go(sankoff_res_kernel<Q, true>);
+  else go(sankoff_res_kernel<Q, false>);
+}
+
 // common entry: validates, fills KArgs, launches one phase
 int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const int8_t* leaves,
               const float* cost, int B, int L, int n_all, int Q, float tau, unsigned flags,
@@ -1143,10 +1282,12 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   }
   if ((int64_t)s.ni * L * Q * 4 > 0x7FFFFFF0LL)
     return set_error(TREX_E_UNSUPPORTED, "%s: one tree's DP table exceeds 2 GiB", fn);
-  const int spt = pick_spt(L, n_slots, s.nl, Q);
+  const size_t lds_res = lds_res_bytes(n_slots, s.nl, s.ni, Q);
+  const bool res = phase == 3 && use_resident(lds_res, B * tiles_for(L, 1));
+  const int spt = res ? 1 : pick_spt(L, n_slots, s.nl, Q);
   const int tiles = tiles_for(L, spt);
-  const size_t lds = lds_bytes(n_slots, s.nl, Q, spt);
-  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
+  const size_t lds = res ? lds_res : lds_bytes(n_slots, s.nl, Q, spt);
+  if (lds > (res ? kLdsPerCu : 65536)) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
   if ((int64_t)B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
   KArgs A;
   A.steps = reinterpret_cast<const int4*>(plan + TREX_PLAN_HEADER_INTS);
@@ -1174,10 +1315,18 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   A.part_dc = A.part_tree + A.nblocks;
   const bool soft = tau > 0.0f;
   hipStream_t st = (hipStream_t)stream;
-  switch (Q) {
-    case 2: dispatch_q<2>(phase, spt, soft, lds, st, A); break;
-    case 3: dispatch_q<3>(phase, spt, soft, lds, st, A); break;
-    case 4: dispatch_q<4>(phase, spt, soft, lds, st, A); break;
+  if (res) {
+    switch (Q) {
+      case 2: launch_res<2>(soft, lds, st, A); break;
+      case 3: launch_res<3>(soft, lds, st, A); break;
+      case 4: launch_res<4>(soft, lds, st, A); break;
+    }
+  } else {
+    switch (Q) {
+      case 2: dispatch_q<2>(phase, spt, soft, lds, st, A); break;
+      case 3: dispatch_q<3>(phase, spt, soft, lds, st, A); break;
+      case 4: dispatch_q<4>(phase, spt, soft, lds, st, A); break;
+    }
   }
   if (int e = hip_check(fn)) return e;
   return partial_reduce(fn, A.part_tree, A.part_dc, B, tiles, Q, phase, tree_score, d_cost, stream);
@@ -1191,9 +1340,12 @@ using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 3; }
+extern "C" int trex_version(void) { return 4; }
 
-extern "C" int trex_dp_site_major(int Q) { return Q > 4 ? 1 : 0; }
+extern "C" int trex_dp_site_major(int Q) {
+  (void)Q;
+  return 1;  // every Q since v4 (Q <= 4 used [n_int][Q][L] before)
+}
 
 extern "C" int64_t trex_workspace_bytes(int B, int L, int n_all, int Q) {
   if (B <= 0 || L <= 0 || Q <= 0) return 0;

@@ -50,6 +50,8 @@ __device__ __forceinline__ bool use_ktrick(float cmin, float cmax, float a) {
 // ---- buffer (SRD) access: 32-bit lane offset in voffset, row offset in
 // soffset, no 64-bit VALU address arithmetic per access ----
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 __device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {

@@ -55,7 +55,7 @@ def leaf_codes(sequences, n_states: int, device=None):
 @dataclass
 class ForwardResult:
     tree_score: "object"  # (B,) float32
-    dp: "object"  # (B, n_int, Q, L) float32 ((B, n_int, L, Q) for Q > 4)
+    dp: "object"  # (B, n_int, L, Q) float32, site-major (trex's per-site rows)
     site_score: "object"  # (B, L) float32 or None
 
 
@@ -83,7 +83,8 @@ class SankoffEngine:
     # -- shapes ------------------------------------------------------------
     @property
     def site_major(self) -> bool:
-        """Q > 4 tables are site-major (lane-per-state kernels, trex_hip.h)."""
+        """DP / marginal tables are site-major (B, n_int, L, Q) for every Q
+        (trex_dp_site_major, include/trex_hip.h)."""
         return bool(lib().trex_dp_site_major(self.Q))
 
     @property
@@ -91,6 +92,11 @@ class SankoffEngine:
         if self.site_major:
             return (self.plan.B, self.plan.n_int, self.L, self.Q)
         return (self.plan.B, self.plan.n_int, self.Q, self.L)
+
+    def state_rows(self, table):
+        """(B, n_int, Q, L) view of a DP / marginal table (the oracle's
+        node-state-site order)."""
+        return table.transpose(2, 3) if self.site_major else table
 
     def _check_inputs(self, leaves, cost):
         torch = _torch()
