@@ -235,6 +235,45 @@ int trex_adam_step(float* params, const float* grads, float* mu, float* nu, int6
                    void* stream);
 int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts, void* stream);
 
+/* ========================================================================
+ * NK landscape-aware loss (src/trex/evals/benchmark.py): the parental
+ * guidance term of _compute_loss_landscape_aware_stacked (:235-306) on top
+ * of the surrogate cost, with compute_parental_logits (:586-663).
+ *   S            fp32 [N][L][Q]  soft sequences (after update_seq)
+ *   interactions int32 [L][k]    epistatic partners, k = interactions.shape[1]
+ *   fitness      fp32 [L][Q^(k+1)], index s * Q^k + sum_j c_j Q^(k-1-j)
+ *                (the site's own state most significant, then neighbour 0:
+ *                the reference's reshape(n_states, -1), :647)
+ * Limits: Q <= 32, k <= 8, k * Q <= 128.
+ * ---------------------------------------------------------------------- */
+
+/* logits [R][L][Q] of parent rows rows[0..R) of S (compute_parental_logits;
+ * k = 0 returns the (L, Q) table per row, :612-620). */
+int trex_nk_parental_logits(const float* S, const int32_t* rows, int R, int L, int Q,
+                            const int32_t* interactions, int k, const float* fitness,
+                            float* logits, void* stream);
+
+/* Host planner, once per (parent map, landscape): parent[n] = argmax_j
+ * A[n][j] (benchmark.py:286, first index).  info[0] = number of distinct
+ * parent rows (n_parents), info[1] = #nodes with parent != self (the
+ * cross-entropy normaliser, :302). Copy the plan to the device. */
+int64_t trex_nk_plan_ints(int N, int L, int k);
+int trex_nk_plan_build(const int32_t* parent, int N, const int32_t* interactions, int L, int k,
+                       int32_t* plan, int32_t* info);
+int64_t trex_nk_workspace_bytes(int N, int L, int Q, int k, int n_parents);
+
+/* loss = surrogate[0] + lambda * CE / (n_nonroot * n_valid) with CE the
+ * masked cross-entropy of every node's sequence against log_softmax of its
+ * parent's logits (:288-302).  seq_mask fp32 [L] (1 valid / 0) or NULL;
+ * n_valid = sum(seq_mask) (L when NULL).  d_S (optional) [N][L][Q] =
+ * d_S_in (optional: e.g. the surrogate's gradient) + d(lambda * fitness)/dS
+ * through both the child and the parent role. */
+int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const float* S, int N, int L,
+                           int Q, const int32_t* interactions, int k, const float* fitness,
+                           const float* seq_mask, float n_valid, float lambda_val, int n_nonroot,
+                           const float* surrogate, const float* d_S_in, float* loss, float* d_S,
+                           void* workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,155 @@
+"""GPU parity of the NK landscape-aware path (trex_nk_*) vs the fp64 oracle
+(oracle/nk_ref.py; reference src/trex/evals/benchmark.py:235-306, 586-663).
+
+Tolerances: logits are fp32 sums of Q^k products of probabilities and table
+entries, accumulated in a fixed order: rtol 1e-5; one-hot parents reproduce
+the table entries exactly.  Loss and gradients: rtol 1e-5 (gradients: atol
+1e-5 * max|g|).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nk_ref as nk
+from trex_amd import nk as NK
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def _n(x):
+    return x.detach().cpu().numpy().astype(np.float64)
+
+
+def _case(n_leaves, L, Q, k, seed, mask=False, root_self=False):
+    rng = np.random.default_rng(seed)
+    n_all = 2 * n_leaves - 1
+    inter, F = nk.random_landscape(L, k, Q, seed=seed + 1)
+    leaves = rng.integers(0, Q, size=(n_leaves, L))
+    A = np.zeros((n_all, n_all), np.float32)
+    par = n_leaves + np.arange(n_all - 1) // 2
+    A[np.arange(n_all - 1), par] = 1.0
+    if root_self:
+        A[-1, -1] = 1.0  # trex's update_tree convention (tree.py:104)
+    anc = rng.normal(size=(n_all - n_leaves, L, Q)).astype(np.float32)
+    m = (rng.random(L) > 0.25) if mask else None
+    S0 = np.zeros((n_all, L, Q), np.float32)
+    S0[np.arange(n_leaves)[:, None], np.arange(L)[None, :], leaves] = 1.0
+    return dict(S0=S0, A=A, inter=inter, F=F, anc=anc, mask=m, n_leaves=n_leaves,
+                leaves=leaves, n_all=n_all)
+
+
+@pytest.mark.parametrize("Q,k,P,L", [(4, 2, 7, 33), (4, 4, 70, 20), (20, 2, 5, 9), (2, 6, 3, 40),
+                                     (20, 1, 65, 12), (3, 3, 1, 1)])
+def test_parental_logits_vs_oracle(device, Q, k, P, L):
+    rng = np.random.default_rng(Q * 100 + k)
+    inter, F = nk.random_landscape(L, k, Q, seed=k)
+    seqs = rng.dirichlet(np.ones(Q), size=(P, L)).astype(np.float32)
+    land = NK.NKLandscape(inter, F, Q, device)
+    out = _n(NK.compute_parental_logits(torch.as_tensor(seqs, device=device), land, k))
+    ref = nk.compute_parental_logits(seqs.astype(np.float64), inter, F.astype(np.float64), k)
+    np.testing.assert_allclose(out, ref, rtol=RTOL, atol=1e-6)
+
+
+def test_parental_logits_one_hot_exact(device):
+    Q, k, L, P = 4, 3, 17, 9
+    rng = np.random.default_rng(0)
+    inter, F = nk.random_landscape(L, k, Q, seed=2)
+    seqs = np.eye(Q, dtype=np.float32)[rng.integers(0, Q, size=(P, L))]
+    land = NK.NKLandscape(inter, F, Q, device)
+    out = NK.compute_parental_logits(torch.as_tensor(seqs, device=device), land, k)
+    ref = nk.compute_parental_logits(seqs.astype(np.float64), inter, F.astype(np.float64), k)
+    np.testing.assert_array_equal(out.cpu().numpy(), ref.astype(np.float32))
+
+
+def test_parental_logits_k0_and_padded(device):
+    L, Q = 10, 4
+    F0 = np.random.default_rng(1).uniform(size=(L, Q)).astype(np.float32)
+    seqs = np.random.default_rng(2).dirichlet(np.ones(Q), size=(3, L)).astype(np.float32)
+    land0 = NK.NKLandscape(np.zeros((L, 0), np.int32), F0, Q, device)
+    out = NK.compute_parental_logits(torch.as_tensor(seqs, device=device), land0, 0)
+    np.testing.assert_array_equal(out.cpu().numpy(), np.broadcast_to(F0, (3, L, Q)))
+    # padded landscape (padding.py:144-216): k_eff = padded k, as the reference
+    inter, F = nk.random_landscape(L, 2, Q, seed=4)
+    ip, Fp = nk.pad_landscape(inter, F, 3, Q)
+    landp = NK.NKLandscape(ip, Fp, Q, device)
+    out = _n(NK.compute_parental_logits(torch.as_tensor(seqs, device=device), landp, 2))
+    ref = nk.compute_parental_logits(seqs.astype(np.float64), ip, Fp.astype(np.float64), 2)
+    np.testing.assert_allclose(out, ref, rtol=RTOL, atol=1e-6)
+
+
+@pytest.mark.parametrize("n_leaves,L,Q,k,mask,root_self",
+                         [(4, 12, 4, 2, False, False), (8, 30, 4, 3, True, False),
+                          (16, 20, 20, 1, True, True), (5, 7, 3, 2, False, True)])
+def test_landscape_loss_and_grad_vs_oracle(device, n_leaves, L, Q, k, mask, root_self):
+    c = _case(n_leaves, L, Q, k, seed=L + Q, mask=mask, root_self=root_self)
+    land = NK.NKLandscape(c["inter"], c["F"], Q, device)
+    lam, T = 0.8, 1.0
+    fn = NK.LandscapeAwareLoss(c["A"], n_leaves, land, lam, k, temperature=T,
+                               seq_mask=c["mask"])
+    loss, g = fn.value_and_grad(torch.as_tensor(c["anc"], device=device),
+                                torch.as_tensor(c["S0"], device=device))
+    rl, rg = nk.landscape_loss_grad(c["anc"].astype(np.float64), c["S0"].astype(np.float64),
+                                    n_leaves, c["inter"], c["F"].astype(np.float64), c["A"], lam,
+                                    k, T, c["mask"])
+    np.testing.assert_allclose(float(loss[0]), rl, rtol=RTOL)
+    np.testing.assert_allclose(_n(g), rg, rtol=RTOL, atol=RTOL * np.abs(rg).max())
+    # functional form == class
+    lf = NK.landscape_aware_loss(torch.as_tensor(c["anc"], device=device),
+                                 torch.as_tensor(c["S0"], device=device), n_leaves, land, c["A"],
+                                 c["n_all"], lam, k, T, c["mask"])
+    assert float(lf) == float(loss[0])
+
+
+def test_landscape_loss_real_k0_is_surrogate(device):
+    c = _case(4, 9, 4, 2, seed=3)
+    land = NK.NKLandscape(c["inter"], c["F"], 4, device)
+    fn = NK.LandscapeAwareLoss(c["A"], 4, land, 0.5, 0)
+    loss, g = fn.value_and_grad(torch.as_tensor(c["anc"], device=device),
+                                torch.as_tensor(c["S0"], device=device))
+    rl, rg = nk.landscape_loss_grad(c["anc"].astype(np.float64), c["S0"].astype(np.float64), 4,
+                                    c["inter"], c["F"], c["A"], 0.5, 0)
+    np.testing.assert_allclose(float(loss[0]), rl, rtol=RTOL)
+    np.testing.assert_allclose(_n(g), rg, rtol=RTOL, atol=RTOL * np.abs(rg).max())
+
+
+def test_landscape_loss_deterministic(device):
+    c = _case(16, 64, 4, 3, seed=11, mask=True)
+    land = NK.NKLandscape(c["inter"], c["F"], 4, device)
+    fn = NK.LandscapeAwareLoss(c["A"], 16, land, 1.0, 3, seq_mask=c["mask"])
+    a = torch.as_tensor(c["anc"], device=device)
+    s = torch.as_tensor(c["S0"], device=device)
+    l1, g1 = fn.value_and_grad(a, s)
+    l1, g1 = l1.clone(), g1.clone()
+    l2, g2 = fn.value_and_grad(a, s)
+    assert torch.equal(l1, l2) and torch.equal(g1, g2)
+
+
+def test_run_landscape_aware_adam_matches_oracle_loop(device):
+    """A few Adam steps on device vs the same loop on the oracle (optax adam
+    semantics, tree_ref.adam_step), then argmax reconstruction."""
+    from oracle import tree_ref as T
+
+    c = _case(4, 10, 4, 2, seed=21)
+    land = NK.NKLandscape(c["inter"], c["F"], 4, device)
+    steps, lr = 5, 0.05
+    out, losses = NK.run_trex_landscape_aware_configurable(
+        c["leaves"], c["n_all"], 4, 4, land, 0.6, c["A"], c["anc"], real_k=2,
+        learning_rate=lr, n_iterations=steps, return_losses=True)
+    p = c["anc"].astype(np.float64)
+    state = T.adam_init({"ancestors": p})
+    ref_losses = []
+    for _ in range(steps):
+        l, g = nk.landscape_loss_grad(p, c["S0"].astype(np.float64), 4, c["inter"],
+                                      c["F"].astype(np.float64), c["A"], 0.6, 2)
+        ref_losses.append(l)
+        upd, state = T.adam_update({"ancestors": g}, state, lr)
+        p = p + upd["ancestors"]
+    np.testing.assert_allclose(_n(losses), ref_losses, rtol=1e-4)
+    top2 = np.sort(p, axis=-1)[..., -2:]  # skip near-ties in the argmax
+    clear = (top2[..., 1] - top2[..., 0]) > 1e-3
+    np.testing.assert_array_equal(out.cpu().numpy()[clear], p.argmax(-1)[clear])

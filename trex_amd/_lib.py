@@ -57,6 +57,13 @@ SIGNATURES = {
     "trex_tree_gram_skip": (_c_i, [_p, _c_i, _c_i64, _c_i, _p, _p, _c_i64, _p]),
     "trex_tree_surrogate_combine": (_c_i, [_p, _p, _c_i, _p, _p, _p, _p, _p]),
     "trex_tree_mf": (_c_i, [_p, _p, _c_i, _c_i64, _p, _p]),
+    # NK landscape-aware loss
+    "trex_nk_parental_logits": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _p, _c_i, _p, _p, _p]),
+    "trex_nk_plan_ints": (_c_i64, [_c_i, _c_i, _c_i]),
+    "trex_nk_plan_build": (_c_i, [_p, _c_i, _p, _c_i, _c_i, _p, _p]),
+    "trex_nk_workspace_bytes": (_c_i64, [_c_i, _c_i, _c_i, _c_i, _c_i]),
+    "trex_nk_landscape_loss": (_c_i, [_p, _c_i, _p, _c_i, _c_i, _c_i, _p, _c_i, _p, _p, _c_f,
+                                      _c_f, _c_i, _p, _p, _p, _p, _p, _c_i64, _p]),
     "trex_tree_mf_rows": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _p, _p]),
     "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),
     "trex_tree_constraint": (_c_i, [_p, _c_i, _c_f, _c_f, _p, _c_i, _p, _p, _p]),

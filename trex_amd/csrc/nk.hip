@@ -1,0 +1,509 @@
+// NK landscape-aware loss on MI355X (gfx950): parental logits, the masked
+// cross-entropy against the children, and the reverse sweep.
+//
+// Reference semantics (maraxen/trex):
+//   compute_parental_logits               src/trex/evals/benchmark.py:586-663
+//   _compute_loss_landscape_aware_stacked src/trex/evals/benchmark.py:235-306
+//
+// logits[p, i, s] = sum_idx F[i][s * Q^k + idx] * prod_j P[p, nb_j(i), c_j(idx)]
+// with idx = sum_j c_j Q^(k-1-j) (neighbour 0 most significant: the
+// reference's successive outer products, :637-642, and the (Q, Q^k) reshape of
+// the site's table, :647).  k = interactions.shape[1] (padded k, :619).
+//
+// Layout: sequences S fp32 [N][L][Q] (node-major, the tree path's layout),
+// interactions int32 [L][k], fitness fp32 [L][Q^(k+1)].
+//
+// Kernel mapping (one wave = 64 parent rows of one site): the site's index
+// set (its neighbours) and its fitness table are wave-uniform, so the table
+// is read with scalar loads and the odometer over the joint index lives in
+// SGPRs; each lane gathers its parent's k neighbour distributions into a
+// per-lane LDS block [j][c][lane] (conflict-free) and walks the Q^k joint
+// states.  The reverse sweep re-walks them: dJ[idx] = sum_s g_s F[s][idx],
+// G[j][c_j] += dJ[idx] * prod_{j' != j} P_j'[c_j'] (prefix / suffix products),
+// written per (parent, site, j); a gather kernel then sums G over the
+// (site, j) pairs that name each neighbour site (inverse-interaction CSR from
+// the host plan) -- fixed order, no atomics, bitwise reproducible.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "sankoff_dev.h"
+#include "trex_common.h"
+
+namespace trex {
+namespace {
+
+constexpr int kNkMaxQ = 32;
+constexpr int kNkMaxK = 8;
+constexpr int32_t kNkMagic = 0x4E4B504C;  // 'NKPL'
+
+int nk_err(const char* fn) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return TREX_OK;
+}
+
+struct NkArgs {
+  const float* S;         // [N][L][Q]
+  const int32_t* rows;    // [R] parent rows of S
+  const int32_t* inter;   // [L][k]
+  const float* F;         // [L][Q^(k+1)]
+  int R, L, Q, k, QK;     // QK = Q^k
+};
+
+// per-lane LDS block: P_j[c] at ((j * Q + c) * 64 + lane)
+__device__ __forceinline__ void gather_neighbours(const NkArgs& a, int row, int site, int lane,
+                                                  bool active, float* pl) {
+  const cptr<int32_t> inter = as_const(a.inter) + (size_t)site * a.k;
+  for (int j = 0; j < a.k; ++j) {
+    const int nb = inter[j];
+    const float* src = a.S + ((size_t)row * a.L + nb) * a.Q;
+    for (int c = 0; c < a.Q; ++c) pl[(j * a.Q + c) * kWave + lane] = active ? src[c] : 0.0f;
+  }
+}
+
+// joint probability of the (uniform) digit vector d and, when WANT_EXCL,
+// prod_{j' != j} for every j (prefix / suffix products)
+template <bool WANT_EXCL>
+__device__ __forceinline__ float joint(const float* pl, int lane, int k, int Q, const int (&d)[kNkMaxK],
+                                       float (&excl)[kNkMaxK]) {
+  float f[kNkMaxK];
+#pragma unroll
+  for (int j = 0; j < kNkMaxK; ++j) f[j] = j < k ? pl[(j * Q + d[j]) * kWave + lane] : 1.0f;
+  float prod = 1.0f;
+  if constexpr (WANT_EXCL) {
+    float pre = 1.0f;
+#pragma unroll
+    for (int j = 0; j < kNkMaxK; ++j) {
+      excl[j] = pre;
+      pre *= f[j];
+    }
+    float suf = 1.0f;
+#pragma unroll
+    for (int j = kNkMaxK - 1; j >= 0; --j) {
+      excl[j] *= suf;
+      suf *= f[j];
+    }
+    prod = pre;
+  } else {
+    // left-to-right, the order of the reference's outer products
+#pragma unroll
+    for (int j = 0; j < kNkMaxK; ++j) prod = j == 0 ? f[0] : prod * f[j];
+  }
+  return prod;
+}
+
+__device__ __forceinline__ void odometer_next(int (&d)[kNkMaxK], int k, int Q) {
+  for (int j = k - 1; j >= 0; --j) {
+    if (++d[j] < Q) return;
+    d[j] = 0;
+  }
+}
+
+// logits [R][L][Q]; grid (ceil(R/64), L)
+__global__ __launch_bounds__(kWave) void nk_logits_kernel(NkArgs a, float* __restrict__ logits) {
+  extern __shared__ __attribute__((aligned(16))) float pl[];
+  const int lane = threadIdx.x;
+  const int site = blockIdx.y;
+  const int r = blockIdx.x * kWave + lane;
+  const bool active = r < a.R;
+  const int row = active ? a.rows[r] : 0;
+  gather_neighbours(a, row, site, lane, active, pl);
+  const cptr<float> F = as_const(a.F) + (size_t)site * a.QK * a.Q;
+  float acc[kNkMaxQ];
+#pragma unroll
+  for (int s = 0; s < kNkMaxQ; ++s) acc[s] = 0.0f;
+  int d[kNkMaxK];
+#pragma unroll
+  for (int j = 0; j < kNkMaxK; ++j) d[j] = 0;
+  float excl[kNkMaxK];
+  for (int idx = 0; idx < a.QK; ++idx) {
+    const float p = a.k == 0 ? 1.0f : joint<false>(pl, lane, a.k, a.Q, d, excl);
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s)
+      if (s < a.Q) acc[s] = fmaf(F[(size_t)s * a.QK + idx], p, acc[s]);
+    odometer_next(d, a.k, a.Q);
+  }
+  if (active) {
+    float* o = logits + ((size_t)r * a.L + site) * a.Q;
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s)
+      if (s < a.Q) o[s] = acc[s];
+  }
+}
+
+// reverse: G [R][L][k][Q] = d(sum g * logits)/d P_j  (per site, per slot j)
+__global__ __launch_bounds__(kWave) void nk_logits_bwd_kernel(NkArgs a, const float* __restrict__ g,
+                                                              float* __restrict__ G) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  const int lane = threadIdx.x;
+  const int site = blockIdx.y;
+  const int r = blockIdx.x * kWave + lane;
+  const bool active = r < a.R;
+  const int row = active ? a.rows[r] : 0;
+  float* pl = sh;
+  float* gl = sh + (size_t)a.k * a.Q * kWave;  // accumulators [j][c][lane]
+  gather_neighbours(a, row, site, lane, active, pl);
+  for (int t = 0; t < a.k * a.Q; ++t) gl[t * kWave + lane] = 0.0f;
+  float gs[kNkMaxQ];
+  const float* gp = g + ((size_t)(active ? r : 0) * a.L + site) * a.Q;
+#pragma unroll
+  for (int s = 0; s < kNkMaxQ; ++s) gs[s] = (s < a.Q && active) ? gp[s] : 0.0f;
+  const cptr<float> F = as_const(a.F) + (size_t)site * a.QK * a.Q;
+  int d[kNkMaxK];
+#pragma unroll
+  for (int j = 0; j < kNkMaxK; ++j) d[j] = 0;
+  float excl[kNkMaxK];
+  for (int idx = 0; idx < a.QK; ++idx) {
+    float dj = 0.0f;
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s)
+      if (s < a.Q) dj = fmaf(gs[s], F[(size_t)s * a.QK + idx], dj);
+    (void)joint<true>(pl, lane, a.k, a.Q, d, excl);
+#pragma unroll
+    for (int j = 0; j < kNkMaxK; ++j)
+      if (j < a.k) {
+        float* gg = gl + (j * a.Q + d[j]) * kWave + lane;
+        *gg = fmaf(dj, excl[j], *gg);
+      }
+    odometer_next(d, a.k, a.Q);
+  }
+  if (active) {
+    float* o = G + (((size_t)r * a.L + site) * a.k) * a.Q;
+    for (int t = 0; t < a.k * a.Q; ++t) o[t] = gl[t * kWave + lane];
+  }
+}
+
+// dS_par [R][L][Q]: for neighbour site m, sum over the (site, j) entries
+// naming m (inverse CSR iofs/ient, ascending (site, j)).  One thread per
+// (r, m, q).
+__global__ __launch_bounds__(256) void nk_gather_kernel(const float* __restrict__ G,
+                                                        const int32_t* __restrict__ iofs,
+                                                        const int32_t* __restrict__ ient, int R,
+                                                        int L, int Q, int k,
+                                                        float* __restrict__ dpar) {
+  const int64_t total = (int64_t)R * L * Q;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t % Q);
+    const int64_t rm = t / Q;
+    const int m = (int)(rm % L);
+    const int64_t r = rm / L;
+    float acc = 0.0f;
+    for (int e = iofs[m]; e < iofs[m + 1]; ++e) {
+      const int lj = ient[e];  // site * k + j
+      acc += G[((size_t)r * L * k + lj) * Q + q];
+    }
+    dpar[t] = acc;
+  }
+}
+
+// Cross-entropy of every child against its parent's logits (benchmark.py
+// :292-300).  One lane per (compact parent pc, site).  Writes
+//   dlog[pc][l][:]  = scale * mask_l * sum_children (softmax * sum_s S_n - S_n)
+//   dchild[n][l][:] = -scale * mask_l * log_softmax(logits[pc(n)])
+//   part[pc * L + l] = sum_children -mask_l * sum_s S_n * logp   (fp64)
+__global__ __launch_bounds__(256) void nk_ce_kernel(const float* __restrict__ S,
+                                                    const float* __restrict__ logits,
+                                                    const int32_t* __restrict__ cofs,
+                                                    const int32_t* __restrict__ cidx,
+                                                    const float* __restrict__ mask, int nP, int L,
+                                                    int Q, float scale, float* __restrict__ dlog,
+                                                    float* __restrict__ dchild,
+                                                    double* __restrict__ part) {
+  const int64_t total = (int64_t)nP * L;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int l = (int)(t % L);
+    const int pc = (int)(t / L);
+    const float* x = logits + (size_t)t * Q;
+    float xv[kNkMaxQ];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s) {
+      xv[s] = s < Q ? x[s] : -INFINITY;
+      mx = fmaxf(mx, xv[s]);
+    }
+    float se = 0.0f;
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s)
+      if (s < Q) se += expf(xv[s] - mx);
+    const float lse = mx + logf(se);
+    const float mk = mask ? mask[l] : 1.0f;
+    float dl[kNkMaxQ];
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s) dl[s] = 0.0f;
+    double ce = 0.0;
+    for (int e = cofs[pc]; e < cofs[pc + 1]; ++e) {
+      const int n = cidx[e];
+      const float* sn = S + ((size_t)n * L + l) * Q;
+      float* dc = dchild + ((size_t)n * L + l) * Q;
+      float tot = 0.0f, cen = 0.0f;
+#pragma unroll
+      for (int s = 0; s < kNkMaxQ; ++s)
+        if (s < Q) {
+          const float v = sn[s];
+          const float lp = xv[s] - lse;
+          tot += v;
+          cen -= v * lp;
+          dc[s] = -scale * mk * lp;
+          dl[s] -= v;
+        }
+#pragma unroll
+      for (int s = 0; s < kNkMaxQ; ++s)
+        if (s < Q) dl[s] += expf(xv[s] - lse) * tot;
+      ce += (double)(mk * cen);
+    }
+    float* dlo = dlog + (size_t)t * Q;
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s)
+      if (s < Q) dlo[s] = scale * mk * dl[s];
+    part[t] = ce;
+  }
+}
+
+// fixed-order sum of the CE partials; loss = surrogate + lambda * ce / norm
+__global__ __launch_bounds__(256) void nk_loss_kernel(const double* __restrict__ part, int64_t n,
+                                                      const float* __restrict__ surrogate,
+                                                      double coef, float* __restrict__ loss) {
+  __shared__ double red[256];
+  double v = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) v += part[i];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)((surrogate ? (double)surrogate[0] : 0.0) + coef * red[0]);
+}
+
+// dS = dS_in + dchild + dpar[rowmap[n]]   (rowmap -1: not a parent)
+__global__ __launch_bounds__(256) void nk_combine_kernel(const float* __restrict__ din,
+                                                         const float* __restrict__ dchild,
+                                                         const float* __restrict__ dpar,
+                                                         const int32_t* __restrict__ rowmap,
+                                                         int N, int L, int Q,
+                                                         float* __restrict__ dout) {
+  const int64_t per = (int64_t)L * Q;
+  const int64_t total = (int64_t)N * per;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(t / per);
+    const int64_t w = t - (int64_t)n * per;
+    const int pc = rowmap[n];
+    float v = (din ? din[t] : 0.0f) + dchild[t];
+    if (pc >= 0) v += dpar[(int64_t)pc * per + w];
+    dout[t] = v;
+  }
+}
+
+int64_t ipow(int b, int e) {
+  int64_t r = 1;
+  for (int i = 0; i < e; ++i) r *= b;
+  return r;
+}
+
+int nk_check(const char* fn, int L, int Q, int k) {
+  if (L <= 0 || Q < 2 || Q > kNkMaxQ || k < 0 || k > kNkMaxK)
+    return set_error(TREX_E_ARG, "%s: bad shape L=%d Q=%d k=%d (Q <= %d, k <= %d)", fn, L, Q, k,
+                     kNkMaxQ, kNkMaxK);
+  if (k * Q > 128)  // per-lane LDS blocks: 2 * k * Q * 64 * 4 B <= 64 KiB
+    return set_error(TREX_E_UNSUPPORTED, "%s: k * Q = %d > 128 not supported", fn, k * Q);
+  if (ipow(Q, k + 1) > (1LL << 26))
+    return set_error(TREX_E_UNSUPPORTED, "%s: fitness table Q^(k+1) too large", fn);
+  return TREX_OK;
+}
+
+int grid1d(int64_t n, int block) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + block - 1) / block, 1 << 16)); }
+
+// plan header ints
+constexpr int kNkHeader = 16;
+
+struct NkPlanView {
+  int N, L, k, nP, n_nonroot;
+  const int32_t *prow, *cofs, *cidx, *rowmap, *iofs, *ient;
+};
+
+NkPlanView plan_view(const int32_t* plan, int N, int L, int k, int nP) {
+  NkPlanView v;
+  v.N = N;
+  v.L = L;
+  v.k = k;
+  v.nP = nP;
+  v.n_nonroot = 0;
+  const int32_t* p = plan + kNkHeader;
+  v.prow = p;
+  p += N;  // room for N distinct parents
+  v.cofs = p;
+  p += N + 1;
+  v.cidx = p;
+  p += N;
+  v.rowmap = p;
+  p += N;
+  v.iofs = p;
+  p += L + 1;
+  v.ient = p;
+  return v;
+}
+
+}  // namespace
+}  // namespace trex
+
+using namespace trex;
+
+extern "C" int64_t trex_nk_plan_ints(int N, int L, int k) {
+  if (N <= 0 || L <= 0 || k < 0) return 0;
+  return kNkHeader + 4LL * N + 1 + (L + 1) + (int64_t)L * k;
+}
+
+extern "C" int trex_nk_plan_build(const int32_t* parent, int N, const int32_t* interactions,
+                                  int L, int k, int32_t* plan, int32_t* info) {
+  if (!parent || !plan || N <= 0 || L <= 0 || k < 0 || k > kNkMaxK || (k > 0 && !interactions))
+    return set_error(TREX_E_ARG, "trex_nk_plan_build: bad arguments (N=%d L=%d k=%d)", N, L, k);
+  for (int n = 0; n < N; ++n)
+    if (parent[n] < 0 || parent[n] >= N)
+      return set_error(TREX_E_ARG, "trex_nk_plan_build: parent[%d] = %d out of range", n, parent[n]);
+  for (int64_t t = 0; t < (int64_t)L * k; ++t)
+    if (interactions[t] < 0 || interactions[t] >= L)
+      return set_error(TREX_E_ARG, "trex_nk_plan_build: interaction %lld = %d out of range",
+                       (long long)t, interactions[t]);
+  std::memset(plan, 0, sizeof(int32_t) * trex_nk_plan_ints(N, L, k));
+  NkPlanView v = plan_view(plan, N, L, k, 0);
+  int32_t* prow = const_cast<int32_t*>(v.prow);
+  int32_t* cofs = const_cast<int32_t*>(v.cofs);
+  int32_t* cidx = const_cast<int32_t*>(v.cidx);
+  int32_t* rowmap = const_cast<int32_t*>(v.rowmap);
+  int32_t* iofs = const_cast<int32_t*>(v.iofs);
+  int32_t* ient = const_cast<int32_t*>(v.ient);
+  // distinct parent rows (ascending) and their children (ascending)
+  std::vector<int> cnt(N, 0);
+  int nonroot = 0;
+  for (int n = 0; n < N; ++n) {
+    cnt[parent[n]] += 1;
+    nonroot += parent[n] != n;
+  }
+  int nP = 0;
+  for (int p = 0; p < N; ++p) {
+    rowmap[p] = cnt[p] > 0 ? nP : -1;
+    if (cnt[p] > 0) prow[nP++] = p;
+  }
+  cofs[0] = 0;
+  for (int i = 0; i < nP; ++i) cofs[i + 1] = cofs[i] + cnt[prow[i]];
+  std::vector<int> fill(nP, 0);
+  for (int n = 0; n < N; ++n) {
+    const int pc = rowmap[parent[n]];
+    cidx[cofs[pc] + fill[pc]++] = n;
+  }
+  // inverse interactions: entries (site*k + j) grouped by the named site
+  std::vector<int> icnt(L, 0);
+  for (int64_t t = 0; t < (int64_t)L * k; ++t) icnt[interactions[t]] += 1;
+  iofs[0] = 0;
+  for (int m = 0; m < L; ++m) iofs[m + 1] = iofs[m] + icnt[m];
+  std::vector<int> ifill(L, 0);
+  for (int64_t t = 0; t < (int64_t)L * k; ++t) {
+    const int m = interactions[t];
+    ient[iofs[m] + ifill[m]++] = (int32_t)t;
+  }
+  plan[0] = kNkMagic;
+  plan[1] = N;
+  plan[2] = L;
+  plan[3] = k;
+  plan[4] = nP;
+  plan[5] = nonroot;
+  if (info) {
+    info[0] = nP;
+    info[1] = nonroot;
+  }
+  return TREX_OK;
+}
+
+extern "C" int64_t trex_nk_workspace_bytes(int N, int L, int Q, int k, int n_parents) {
+  if (N <= 0 || L <= 0 || Q <= 0 || k < 0 || n_parents <= 0) return 0;
+  const int64_t per = (int64_t)L * Q;
+  int64_t b = 0;
+  b += (int64_t)n_parents * per * 4;      // logits
+  b += (int64_t)n_parents * per * 4;      // dlogits
+  b += (int64_t)N * per * 4;              // dchild
+  b += (int64_t)n_parents * per * k * 4;  // G
+  b += (int64_t)n_parents * per * 4;      // dpar
+  b += (int64_t)n_parents * L * 8;        // CE partials
+  return b + 6 * 256;
+}
+
+extern "C" int trex_nk_parental_logits(const float* seqs, const int32_t* rows, int R, int L, int Q,
+                                       const int32_t* interactions, int k, const float* fitness,
+                                       float* logits, void* stream) {
+  const char* fn = "trex_nk_parental_logits";
+  if (int e = nk_check(fn, L, Q, k)) return e;
+  if (!seqs || !rows || R <= 0 || !fitness || !logits || (k > 0 && !interactions))
+    return set_error(TREX_E_ARG, "%s: null pointer / bad R", fn);
+  NkArgs a{seqs, rows, interactions, fitness, R, L, Q, k, (int)ipow(Q, k)};
+  const size_t lds = std::max<size_t>(16, (size_t)k * Q * kWave * 4);
+  hipLaunchKernelGGL(nk_logits_kernel, dim3((R + kWave - 1) / kWave, L), dim3(kWave), lds,
+                     (hipStream_t)stream, a, logits);
+  return nk_err(fn);
+}
+
+extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const float* seqs, int N,
+                                      int L, int Q, const int32_t* interactions, int k,
+                                      const float* fitness, const float* seq_mask,
+                                      float n_valid, float lambda_val, int n_nonroot,
+                                      const float* surrogate, const float* d_seqs_in, float* loss,
+                                      float* d_seqs, void* workspace, int64_t workspace_bytes,
+                                      void* stream) {
+  const char* fn = "trex_nk_landscape_loss";
+  if (int e = nk_check(fn, L, Q, k)) return e;
+  if (!plan || !seqs || !fitness || !loss || !workspace || n_parents <= 0 || N <= 0 ||
+      (k > 0 && !interactions))
+    return set_error(TREX_E_ARG, "%s: null pointer / bad sizes", fn);
+  if (workspace_bytes < trex_nk_workspace_bytes(N, L, Q, k, n_parents))
+    return set_error(TREX_E_ARG, "%s: workspace too small", fn);
+  if (!(n_valid > 0.0f) || n_nonroot <= 0)
+    return set_error(TREX_E_ARG, "%s: empty normaliser (n_valid=%g, n_nonroot=%d)", fn, n_valid,
+                     n_nonroot);
+  hipStream_t st = (hipStream_t)stream;
+  const NkPlanView v = plan_view(plan, N, L, k, n_parents);
+  const int64_t per = (int64_t)L * Q;
+  auto carve = [&](char*& p, int64_t bytes) {
+    char* r = p;
+    p += (bytes + 255) / 256 * 256;
+    return r;
+  };
+  char* w = static_cast<char*>(workspace);
+  float* logits = reinterpret_cast<float*>(carve(w, (int64_t)n_parents * per * 4));
+  float* dlog = reinterpret_cast<float*>(carve(w, (int64_t)n_parents * per * 4));
+  float* dchild = reinterpret_cast<float*>(carve(w, (int64_t)N * per * 4));
+  float* G = reinterpret_cast<float*>(carve(w, (int64_t)n_parents * per * k * 4));
+  float* dpar = reinterpret_cast<float*>(carve(w, (int64_t)n_parents * per * 4));
+  double* part = reinterpret_cast<double*>(carve(w, (int64_t)n_parents * L * 8));
+
+  NkArgs a{seqs, v.prow, interactions, fitness, n_parents, L, Q, k, (int)ipow(Q, k)};
+  const size_t lds = std::max<size_t>(16, (size_t)k * Q * kWave * 4);
+  hipLaunchKernelGGL(nk_logits_kernel, dim3((n_parents + kWave - 1) / kWave, L), dim3(kWave), lds,
+                     st, a, logits);
+  if (int e = nk_err(fn)) return e;
+  const double norm = (double)n_nonroot * (double)n_valid;
+  const float scale = (float)((double)lambda_val / norm);
+  hipLaunchKernelGGL(nk_ce_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
+                     seqs, logits, v.cofs, v.cidx, seq_mask, n_parents, L, Q, scale, dlog, dchild,
+                     part);
+  hipLaunchKernelGGL(nk_loss_kernel, dim3(1), dim3(256), 0, st, part, (int64_t)n_parents * L,
+                     surrogate, (double)lambda_val / norm, loss);
+  if (int e = nk_err(fn)) return e;
+  if (!d_seqs) return TREX_OK;
+  if (k > 0) {
+    hipLaunchKernelGGL(nk_logits_bwd_kernel, dim3((n_parents + kWave - 1) / kWave, L), dim3(kWave),
+                       2 * lds, st, a, dlog, G);
+    hipLaunchKernelGGL(nk_gather_kernel, dim3(grid1d((int64_t)n_parents * per, 256)), dim3(256), 0,
+                       st, G, v.iofs, v.ient, n_parents, L, Q, k, dpar);
+  } else {
+    (void)hipMemsetAsync(dpar, 0, (size_t)n_parents * per * 4, st);
+  }
+  hipLaunchKernelGGL(nk_combine_kernel, dim3(grid1d((int64_t)N * per, 256)), dim3(256), 0, st,
+                     d_seqs_in, dchild, dpar, v.rowmap, N, L, Q, d_seqs);
+  return nk_err(fn);
+}
