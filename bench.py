@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 single-tree line")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 protein line")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 tree-cost loop line")
+    ap.add_argument("--no-nk", action="store_true", help="skip the NK landscape-aware line")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/pmc_traffic.py)")
@@ -303,6 +304,50 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
             "trex_equivalent_gemm_tflops": flops / sec / 1e12, "loss_last": float(loss)}
 
 
+def nk_line(torch, device, steps=50, warmup=5):
+    """the NK landscape-aware objective
+    (src/trex/evals/benchmark.py:235-306, 586-663) -- one Adam step of
+    run_trex_landscape_aware_configurable (loss + grad + optax adam), at the
+    reference's eval shape (benchmark.py:981-985: 32 leaves, N = 15 sites,
+    binary states, K = 10, lambda = 3) and at a larger DNA shape."""
+    from oracle.nk_ref import random_landscape  # synthetic landscape (shapes only)
+    from trex_amd import nk as NK
+    from trex_amd.tree import Adam
+
+    out = {}
+    for name, (nl, L, Q, k, lam) in {"eval_32x15_q2_k10": (32, 15, 2, 10, 3.0),
+                                     "dna_256x2000_q4_k4": (256, 2000, 4, 4, 1.0)}.items():
+        n_all = 2 * nl - 1
+        rng = np.random.default_rng(8)
+        inter, F = random_landscape(L, k, Q, seed=9)
+        A = np.zeros((n_all, n_all), np.float32)
+        A[np.arange(n_all - 1), nl + np.arange(n_all - 1) // 2] = 1.0
+        land = NK.NKLandscape(inter, F, Q, device)
+        S0 = NK.masked_sequences_from_leaves(rng.integers(0, Q, size=(nl, L)), n_all, Q, device)
+        fn = NK.LandscapeAwareLoss(A, nl, land, lam, k)
+        params = {"ancestors": torch.as_tensor(rng.normal(size=(nl - 1, L, Q)), dtype=torch.float32,
+                                               device=device)}
+        opt = Adam(params, 1e-3)
+
+        def step():
+            _, g = fn.value_and_grad(params["ancestors"], S0)
+            opt.step(params, {"ancestors": g})
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        sec = (time.perf_counter() - t0) / steps
+        out[name] = {"workload": f"{nl} leaves x {L} sites x {Q} states, K={k}, lambda={lam}: "
+                                 "landscape-aware loss + grad + adam step (eager launches)",
+                     "ms_per_step": sec * 1e3,
+                     "logit_macs_per_step": 2 * fn.n_parents * L * Q ** (k + 1)}
+    return out
+
+
 def cpu_baseline(ch, leaves_np, cost_np, tau, L, n, Q, threads):
     """OpenMP C restatement (oracle/cpu_port.c) on this host's cores, on a
     bounded sample of the same workload; plus the trex-structure numpy proxy."""
@@ -474,6 +519,8 @@ def main():
             result["c3"] = c3_line(torch, device, threads)
         if not args.no_c5:
             result["c5"] = c5_line(torch, device)
+        if not args.no_nk:
+            result["nk"] = nk_line(torch, device)
     if world > 1 and not args.no_c5:
         result["c5"] = c5_line(torch, device, rank=rank, world=world)
     if rank == 0:

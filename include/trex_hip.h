@@ -244,7 +244,7 @@ int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts, vo
  *   fitness      fp32 [L][Q^(k+1)], index s * Q^k + sum_j c_j Q^(k-1-j)
  *                (the site's own state most significant, then neighbour 0:
  *                the reference's reshape(n_states, -1), :647)
- * Limits: Q <= 32, k <= 8, k * Q <= 128.
+ * Limits: Q <= 32, k <= 16, k * Q <= 128.
  * ---------------------------------------------------------------------- */
 
 /* logits [R][L][Q] of parent rows rows[0..R) of S (compute_parental_logits;

@@ -44,7 +44,7 @@ def _case(n_leaves, L, Q, k, seed, mask=False, root_self=False):
 
 
 @pytest.mark.parametrize("Q,k,P,L", [(4, 2, 7, 33), (4, 4, 70, 20), (20, 2, 5, 9), (2, 6, 3, 40),
-                                     (20, 1, 65, 12), (3, 3, 1, 1)])
+                                     (20, 1, 65, 12), (3, 3, 1, 1), (2, 10, 63, 15)])
 def test_parental_logits_vs_oracle(device, Q, k, P, L):
     rng = np.random.default_rng(Q * 100 + k)
     inter, F = nk.random_landscape(L, k, Q, seed=k)
@@ -84,7 +84,8 @@ def test_parental_logits_k0_and_padded(device):
 
 @pytest.mark.parametrize("n_leaves,L,Q,k,mask,root_self",
                          [(4, 12, 4, 2, False, False), (8, 30, 4, 3, True, False),
-                          (16, 20, 20, 1, True, True), (5, 7, 3, 2, False, True)])
+                          (16, 20, 20, 1, True, True), (5, 7, 3, 2, False, True),
+                          (32, 15, 2, 10, False, False)])  # benchmark.py:981-985 eval shape
 def test_landscape_loss_and_grad_vs_oracle(device, n_leaves, L, Q, k, mask, root_self):
     c = _case(n_leaves, L, Q, k, seed=L + Q, mask=mask, root_self=root_self)
     land = NK.NKLandscape(c["inter"], c["F"], Q, device)

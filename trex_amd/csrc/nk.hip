@@ -37,7 +37,7 @@ namespace trex {
 namespace {
 
 constexpr int kNkMaxQ = 32;
-constexpr int kNkMaxK = 8;
+constexpr int kNkMaxK = 16;
 constexpr int32_t kNkMagic = 0x4E4B504C;  // 'NKPL'
 
 int nk_err(const char* fn) {
@@ -65,115 +65,204 @@ __device__ __forceinline__ void gather_neighbours(const NkArgs& a, int row, int 
   }
 }
 
-// joint probability of the (uniform) digit vector d and, when WANT_EXCL,
-// prod_{j' != j} for every j (prefix / suffix products)
-template <bool WANT_EXCL>
-__device__ __forceinline__ float joint(const float* pl, int lane, int k, int Q, const int (&d)[kNkMaxK],
-                                       float (&excl)[kNkMaxK]) {
-  float f[kNkMaxK];
-#pragma unroll
-  for (int j = 0; j < kNkMaxK; ++j) f[j] = j < k ? pl[(j * Q + d[j]) * kWave + lane] : 1.0f;
-  float prod = 1.0f;
-  if constexpr (WANT_EXCL) {
-    float pre = 1.0f;
-#pragma unroll
-    for (int j = 0; j < kNkMaxK; ++j) {
-      excl[j] = pre;
-      pre *= f[j];
-    }
-    float suf = 1.0f;
-#pragma unroll
-    for (int j = kNkMaxK - 1; j >= 0; --j) {
-      excl[j] *= suf;
-      suf *= f[j];
-    }
-    prod = pre;
-  } else {
-    // left-to-right, the order of the reference's outer products
-#pragma unroll
-    for (int j = 0; j < kNkMaxK; ++j) prod = j == 0 ? f[0] : prod * f[j];
-  }
-  return prod;
+// The Q^k joint states are walked as (outer, c): outer enumerates the
+// digits of neighbours 0..k-2 (an odometer in uniform registers), c the last
+// neighbour's state, innermost.  Per outer state the prefix product
+// pre = ((f_0 f_1) ... f_{k-2}) -- the association of the reference's
+// successive outer products -- is read from the per-lane LDS block (k - 1
+// reads), and the inner loop needs only the last neighbour's Q values, which
+// stay in registers.  A block holds NS waves that split the outer range
+// (parallelism for few parents / large Q^k); partials are combined in a
+// fixed wave order.
+struct Walk {
+  int k, Q, QK, nouter, o0, o1;  // outer states [o0, o1) of this wave
+};
+
+__device__ __forceinline__ Walk walk_of(const NkArgs& a, int wave, int ns) {
+  Walk w;
+  w.k = a.k;
+  w.Q = a.Q;
+  w.QK = a.QK;
+  w.nouter = a.k == 0 ? 1 : a.QK / a.Q;
+  const int per = (w.nouter + ns - 1) / ns;
+  w.o0 = min(w.nouter, wave * per);
+  w.o1 = min(w.nouter, w.o0 + per);
+  return w;
 }
 
-__device__ __forceinline__ void odometer_next(int (&d)[kNkMaxK], int k, int Q) {
-  for (int j = k - 1; j >= 0; --j) {
+__device__ __forceinline__ void digits_of(int outer, int k, int Q, int (&d)[kNkMaxK]) {
+#pragma unroll
+  for (int j = kNkMaxK - 1; j >= 0; --j) {
+    if (j < k - 1) {
+      d[j] = outer % Q;
+      outer /= Q;
+    } else {
+      d[j] = 0;
+    }
+  }
+}
+
+__device__ __forceinline__ void digits_next(int (&d)[kNkMaxK], int k, int Q) {
+  for (int j = k - 2; j >= 0; --j) {
     if (++d[j] < Q) return;
     d[j] = 0;
   }
 }
 
-// logits [R][L][Q]; grid (ceil(R/64), L)
-__global__ __launch_bounds__(kWave) void nk_logits_kernel(NkArgs a, float* __restrict__ logits) {
-  extern __shared__ __attribute__((aligned(16))) float pl[];
+// logits [R][L][Q]; grid (ceil(R/64), L), block (64, NS)
+// QT: compile-time Q (2, 4, 20) or 0 = runtime Q <= kNkMaxQ
+template <int QT>
+__global__ __launch_bounds__(512) void nk_logits_kernel(NkArgs a, float* __restrict__ logits) {
+  constexpr int MQ = QT ? QT : kNkMaxQ;
+  const int Q = QT ? QT : a.Q;
+  extern __shared__ __attribute__((aligned(16))) float sh[];
   const int lane = threadIdx.x;
+  const int wave = threadIdx.y;
+  const int ns = blockDim.y;
   const int site = blockIdx.y;
   const int r = blockIdx.x * kWave + lane;
   const bool active = r < a.R;
   const int row = active ? a.rows[r] : 0;
-  gather_neighbours(a, row, site, lane, active, pl);
-  const cptr<float> F = as_const(a.F) + (size_t)site * a.QK * a.Q;
-  float acc[kNkMaxQ];
+  float* pl = sh;                                    // [k][Q][64]
+  float* part = sh + (size_t)a.k * Q * kWave;      // [NS][Q][64]
+  if (wave == 0) gather_neighbours(a, row, site, lane, active, pl);
+  __syncthreads();
+  const cptr<float> F = as_const(a.F) + (size_t)site * a.QK * Q;
+  const Walk w = walk_of(a, wave, ns);
+  float last[MQ];  // P_{k-1}[c]
 #pragma unroll
-  for (int s = 0; s < kNkMaxQ; ++s) acc[s] = 0.0f;
+  for (int c = 0; c < MQ; ++c)
+    last[c] = (a.k > 0 && c < Q) ? pl[((a.k - 1) * Q + c) * kWave + lane] : 1.0f;
+  float acc[MQ];
+#pragma unroll
+  for (int s = 0; s < MQ; ++s) acc[s] = 0.0f;
   int d[kNkMaxK];
+  digits_of(w.o0, a.k, Q, d);
+  const int inner = a.k == 0 ? 1 : Q;
+  for (int outer = w.o0; outer < w.o1; ++outer) {
+    float pre = 1.0f;
 #pragma unroll
-  for (int j = 0; j < kNkMaxK; ++j) d[j] = 0;
-  float excl[kNkMaxK];
-  for (int idx = 0; idx < a.QK; ++idx) {
-    const float p = a.k == 0 ? 1.0f : joint<false>(pl, lane, a.k, a.Q, d, excl);
+    for (int j = 0; j < kNkMaxK; ++j) {
+      if (j < a.k - 1) {
+        const float f = pl[(j * Q + d[j]) * kWave + lane];
+        pre = j == 0 ? f : pre * f;
+      }
+    }
+    const int base = outer * inner;
 #pragma unroll
-    for (int s = 0; s < kNkMaxQ; ++s)
-      if (s < a.Q) acc[s] = fmaf(F[(size_t)s * a.QK + idx], p, acc[s]);
-    odometer_next(d, a.k, a.Q);
+    for (int c = 0; c < MQ; ++c) {
+      if (c < inner) {
+        const float p = a.k == 0 ? 1.0f : (a.k == 1 ? last[c] : pre * last[c]);
+#pragma unroll
+        for (int s = 0; s < MQ; ++s)
+          if (s < Q) acc[s] = fmaf(F[(size_t)s * a.QK + base + c], p, acc[s]);
+      }
+    }
+    digits_next(d, a.k, Q);
+  }
+  if (ns > 1) {
+    for (int s = 0; s < Q; ++s) part[((size_t)wave * Q + s) * kWave + lane] = acc[s];
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int s = 0; s < MQ; ++s) {
+      if (s < Q) {
+        float v = part[(size_t)s * kWave + lane];
+        for (int y = 1; y < ns; ++y) v += part[((size_t)y * Q + s) * kWave + lane];
+        acc[s] = v;
+      }
+    }
   }
   if (active) {
-    float* o = logits + ((size_t)r * a.L + site) * a.Q;
+    float* o = logits + ((size_t)r * a.L + site) * Q;
 #pragma unroll
-    for (int s = 0; s < kNkMaxQ; ++s)
-      if (s < a.Q) o[s] = acc[s];
+    for (int s = 0; s < MQ; ++s)
+      if (s < Q) o[s] = acc[s];
   }
 }
 
-// reverse: G [R][L][k][Q] = d(sum g * logits)/d P_j  (per site, per slot j)
-__global__ __launch_bounds__(kWave) void nk_logits_bwd_kernel(NkArgs a, const float* __restrict__ g,
-                                                              float* __restrict__ G) {
+// reverse: G [R][L][k][Q] = d(sum g * logits)/d P_j  (per site, per slot j).
+// Per outer state: E_j = prod_{j' < k-1, j' != j} f_j' (prefix x suffix),
+// inner c: dJ_c = sum_s g_s F[s][outer*Q + c]; G[k-1][c] += dJ_c * pre (in
+// registers); T = sum_c dJ_c P_{k-1}[c]; then G[j][d_j] += E_j * T (LDS).
+template <int QT>
+__global__ __launch_bounds__(512) void nk_logits_bwd_kernel(NkArgs a, const float* __restrict__ g,
+                                                            float* __restrict__ G) {
+  constexpr int MQ = QT ? QT : kNkMaxQ;
+  const int Q = QT ? QT : a.Q;
   extern __shared__ __attribute__((aligned(16))) float sh[];
   const int lane = threadIdx.x;
+  const int wave = threadIdx.y;
+  const int ns = blockDim.y;
   const int site = blockIdx.y;
   const int r = blockIdx.x * kWave + lane;
   const bool active = r < a.R;
   const int row = active ? a.rows[r] : 0;
-  float* pl = sh;
-  float* gl = sh + (size_t)a.k * a.Q * kWave;  // accumulators [j][c][lane]
-  gather_neighbours(a, row, site, lane, active, pl);
-  for (int t = 0; t < a.k * a.Q; ++t) gl[t * kWave + lane] = 0.0f;
-  float gs[kNkMaxQ];
-  const float* gp = g + ((size_t)(active ? r : 0) * a.L + site) * a.Q;
+  const int kq = a.k * Q;
+  float* pl = sh;                                          // [k][Q][64]
+  float* gl = sh + (size_t)kq * kWave * (1 + wave);        // this wave's bins [k][Q][64]
+  if (wave == 0) gather_neighbours(a, row, site, lane, active, pl);
+  for (int t = 0; t < kq; ++t) gl[t * kWave + lane] = 0.0f;
+  __syncthreads();
+  float gs[MQ];
+  const float* gp = g + ((size_t)(active ? r : 0) * a.L + site) * Q;
 #pragma unroll
-  for (int s = 0; s < kNkMaxQ; ++s) gs[s] = (s < a.Q && active) ? gp[s] : 0.0f;
-  const cptr<float> F = as_const(a.F) + (size_t)site * a.QK * a.Q;
+  for (int s = 0; s < MQ; ++s) gs[s] = (s < Q && active) ? gp[s] : 0.0f;
+  const cptr<float> F = as_const(a.F) + (size_t)site * a.QK * Q;
+  const Walk w = walk_of(a, wave, ns);
+  float last[MQ], glast[MQ];
+#pragma unroll
+  for (int c = 0; c < MQ; ++c) {
+    last[c] = c < Q ? pl[((a.k - 1) * Q + c) * kWave + lane] : 0.0f;
+    glast[c] = 0.0f;
+  }
   int d[kNkMaxK];
+  digits_of(w.o0, a.k, Q, d);
+  for (int outer = w.o0; outer < w.o1; ++outer) {
+    float f[kNkMaxK], E[kNkMaxK];
 #pragma unroll
-  for (int j = 0; j < kNkMaxK; ++j) d[j] = 0;
-  float excl[kNkMaxK];
-  for (int idx = 0; idx < a.QK; ++idx) {
-    float dj = 0.0f;
+    for (int j = 0; j < kNkMaxK; ++j) f[j] = j < a.k - 1 ? pl[(j * Q + d[j]) * kWave + lane] : 1.0f;
+    float pre = 1.0f;
 #pragma unroll
-    for (int s = 0; s < kNkMaxQ; ++s)
-      if (s < a.Q) dj = fmaf(gs[s], F[(size_t)s * a.QK + idx], dj);
-    (void)joint<true>(pl, lane, a.k, a.Q, d, excl);
+    for (int j = 0; j < kNkMaxK; ++j) {
+      E[j] = pre;
+      pre *= f[j];
+    }
+    float suf = 1.0f;
+#pragma unroll
+    for (int j = kNkMaxK - 1; j >= 0; --j) {
+      E[j] *= suf;
+      suf *= f[j];
+    }
+    const int base = outer * Q;
+    float T = 0.0f;
+#pragma unroll
+    for (int c = 0; c < MQ; ++c) {
+      if (c < Q) {
+        float dj = 0.0f;
+#pragma unroll
+        for (int s = 0; s < MQ; ++s)
+          if (s < Q) dj = fmaf(gs[s], F[(size_t)s * a.QK + base + c], dj);
+        glast[c] = fmaf(dj, pre, glast[c]);
+        T = fmaf(dj, last[c], T);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kNkMaxK; ++j)
-      if (j < a.k) {
-        float* gg = gl + (j * a.Q + d[j]) * kWave + lane;
-        *gg = fmaf(dj, excl[j], *gg);
+      if (j < a.k - 1) {
+        float* gg = gl + (j * Q + d[j]) * kWave + lane;
+        *gg = fmaf(E[j], T, *gg);
       }
-    odometer_next(d, a.k, a.Q);
+    digits_next(d, a.k, Q);
   }
-  if (active) {
-    float* o = G + (((size_t)r * a.L + site) * a.k) * a.Q;
-    for (int t = 0; t < a.k * a.Q; ++t) o[t] = gl[t * kWave + lane];
+  for (int c = 0; c < Q; ++c) gl[((a.k - 1) * Q + c) * kWave + lane] = glast[c];
+  __syncthreads();
+  if (wave != 0 || !active) return;
+  float* o = G + (((size_t)r * a.L + site) * a.k) * Q;
+  for (int t = 0; t < kq; ++t) {
+    float v = sh[(size_t)kq * kWave + t * kWave + lane];
+    for (int y = 1; y < ns; ++y) v += sh[(size_t)kq * kWave * (1 + y) + t * kWave + lane];
+    o[t] = v;
   }
 }
 
@@ -265,7 +354,27 @@ __global__ __launch_bounds__(256) void nk_ce_kernel(const float* __restrict__ S,
   }
 }
 
-// fixed-order sum of the CE partials; loss = surrogate + lambda * ce / norm
+// fixed-order two-level sum of the CE partials: block b sums chunk b into
+// sums[b]; nk_loss_kernel then sums the chunks and writes
+// loss = surrogate + lambda * ce / norm
+constexpr int kNkChunks = 256;
+__global__ __launch_bounds__(256) void nk_chunk_sum_kernel(const double* __restrict__ part,
+                                                           int64_t n, double* __restrict__ sums) {
+  __shared__ double red[256];
+  const int64_t per = (n + kNkChunks - 1) / kNkChunks;
+  const int64_t lo = (int64_t)blockIdx.x * per;
+  const int64_t hi = min(n, lo + per);
+  double v = 0.0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) v += part[i];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = red[0];
+}
+
 __global__ __launch_bounds__(256) void nk_loss_kernel(const double* __restrict__ part, int64_t n,
                                                       const float* __restrict__ surrogate,
                                                       double coef, float* __restrict__ loss) {
@@ -316,6 +425,45 @@ int nk_check(const char* fn, int L, int Q, int k) {
   if (ipow(Q, k + 1) > (1LL << 26))
     return set_error(TREX_E_UNSUPPORTED, "%s: fitness table Q^(k+1) too large", fn);
   return TREX_OK;
+}
+
+// waves per block splitting the outer joint states: enough waves to fill
+// the chip when there are few (parent-group, site) blocks, each wave with
+// >= 2 outer states, and the bwd's per-wave LDS bins within 64 KiB
+int nk_slices(int R, int L, int Q, int k) {
+  if (k == 0) return 1;
+  const int64_t nouter = ipow(Q, k - 1);
+  const int64_t blocks = (int64_t)((R + kWave - 1) / kWave) * L;
+  int ns = 1;
+  while (ns < 8 && blocks * ns < 4096 && nouter >= 4LL * ns &&
+         (int64_t)(2 + 2 * ns) * k * Q * kWave * 4 <= 65536)
+    ns *= 2;
+  return ns;
+}
+
+size_t nk_fwd_lds(int Q, int k, int ns) { return std::max<size_t>(16, ((size_t)k * Q + (size_t)ns * Q) * kWave * 4); }
+size_t nk_bwd_lds(int Q, int k, int ns) { return std::max<size_t>(16, (size_t)(1 + ns) * k * Q * kWave * 4); }
+
+void launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits) {
+  const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);
+  const size_t lds = nk_fwd_lds(a.Q, a.k, ns);
+  switch (a.Q) {
+    case 2: hipLaunchKernelGGL(nk_logits_kernel<2>, grid, block, lds, st, a, logits); break;
+    case 4: hipLaunchKernelGGL(nk_logits_kernel<4>, grid, block, lds, st, a, logits); break;
+    case 20: hipLaunchKernelGGL(nk_logits_kernel<20>, grid, block, lds, st, a, logits); break;
+    default: hipLaunchKernelGGL(nk_logits_kernel<0>, grid, block, lds, st, a, logits);
+  }
+}
+
+void launch_logits_bwd(const NkArgs& a, int ns, hipStream_t st, const float* g, float* G) {
+  const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);
+  const size_t lds = nk_bwd_lds(a.Q, a.k, ns);
+  switch (a.Q) {
+    case 2: hipLaunchKernelGGL(nk_logits_bwd_kernel<2>, grid, block, lds, st, a, g, G); break;
+    case 4: hipLaunchKernelGGL(nk_logits_bwd_kernel<4>, grid, block, lds, st, a, g, G); break;
+    case 20: hipLaunchKernelGGL(nk_logits_bwd_kernel<20>, grid, block, lds, st, a, g, G); break;
+    default: hipLaunchKernelGGL(nk_logits_bwd_kernel<0>, grid, block, lds, st, a, g, G);
+  }
 }
 
 int grid1d(int64_t n, int block) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + block - 1) / block, 1 << 16)); }
@@ -431,7 +579,8 @@ extern "C" int64_t trex_nk_workspace_bytes(int N, int L, int Q, int k, int n_par
   b += (int64_t)n_parents * per * k * 4;  // G
   b += (int64_t)n_parents * per * 4;      // dpar
   b += (int64_t)n_parents * L * 8;        // CE partials
-  return b + 6 * 256;
+  b += 256 * 8;                           // chunk sums
+  return b + 7 * 256;
 }
 
 extern "C" int trex_nk_parental_logits(const float* seqs, const int32_t* rows, int R, int L, int Q,
@@ -442,9 +591,8 @@ extern "C" int trex_nk_parental_logits(const float* seqs, const int32_t* rows, i
   if (!seqs || !rows || R <= 0 || !fitness || !logits || (k > 0 && !interactions))
     return set_error(TREX_E_ARG, "%s: null pointer / bad R", fn);
   NkArgs a{seqs, rows, interactions, fitness, R, L, Q, k, (int)ipow(Q, k)};
-  const size_t lds = std::max<size_t>(16, (size_t)k * Q * kWave * 4);
-  hipLaunchKernelGGL(nk_logits_kernel, dim3((R + kWave - 1) / kWave, L), dim3(kWave), lds,
-                     (hipStream_t)stream, a, logits);
+  const int ns = nk_slices(R, L, Q, k);
+  launch_logits(a, ns, (hipStream_t)stream, logits);
   return nk_err(fn);
 }
 
@@ -480,24 +628,25 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
   float* G = reinterpret_cast<float*>(carve(w, (int64_t)n_parents * per * k * 4));
   float* dpar = reinterpret_cast<float*>(carve(w, (int64_t)n_parents * per * 4));
   double* part = reinterpret_cast<double*>(carve(w, (int64_t)n_parents * L * 8));
+  double* sums = reinterpret_cast<double*>(carve(w, kNkChunks * 8));
 
   NkArgs a{seqs, v.prow, interactions, fitness, n_parents, L, Q, k, (int)ipow(Q, k)};
-  const size_t lds = std::max<size_t>(16, (size_t)k * Q * kWave * 4);
-  hipLaunchKernelGGL(nk_logits_kernel, dim3((n_parents + kWave - 1) / kWave, L), dim3(kWave), lds,
-                     st, a, logits);
+  const int ns = nk_slices(n_parents, L, Q, k);
+  launch_logits(a, ns, st, logits);
   if (int e = nk_err(fn)) return e;
   const double norm = (double)n_nonroot * (double)n_valid;
   const float scale = (float)((double)lambda_val / norm);
   hipLaunchKernelGGL(nk_ce_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
                      seqs, logits, v.cofs, v.cidx, seq_mask, n_parents, L, Q, scale, dlog, dchild,
                      part);
-  hipLaunchKernelGGL(nk_loss_kernel, dim3(1), dim3(256), 0, st, part, (int64_t)n_parents * L,
+  hipLaunchKernelGGL(nk_chunk_sum_kernel, dim3(kNkChunks), dim3(256), 0, st, part,
+                     (int64_t)n_parents * L, sums);
+  hipLaunchKernelGGL(nk_loss_kernel, dim3(1), dim3(256), 0, st, sums, (int64_t)kNkChunks,
                      surrogate, (double)lambda_val / norm, loss);
   if (int e = nk_err(fn)) return e;
   if (!d_seqs) return TREX_OK;
   if (k > 0) {
-    hipLaunchKernelGGL(nk_logits_bwd_kernel, dim3((n_parents + kWave - 1) / kWave, L), dim3(kWave),
-                       2 * lds, st, a, dlog, G);
+    launch_logits_bwd(a, ns, st, dlog, G);
     hipLaunchKernelGGL(nk_gather_kernel, dim3(grid1d((int64_t)n_parents * per, 256)), dim3(256), 0,
                        st, G, v.iofs, v.ient, n_parents, L, Q, k, dpar);
   } else {
