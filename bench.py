@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 protein line")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 tree-cost loop line")
     ap.add_argument("--no-nk", action="store_true", help="skip the NK landscape-aware line")
+    ap.add_argument("--no-ragged", action="store_true", help="skip the ragged-batch line")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/pmc_traffic.py)")
@@ -304,6 +305,38 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
             "trex_equivalent_gemm_tflops": flops / sec / 1e12, "loss_last": float(loss)}
 
 
+def ragged_line(torch, device, steps=20, warmup=3):
+    """a ragged C4-like batch -- 128 random topologies
+    with 8..64 taxa and 1 000..5 000 sites each, softmin tau=0.5 fwd + grad in
+    one launch (trex pads such a batch to MAX_NODES / N buckets,
+    padding.py:25-27)."""
+    from trex_amd import random_topologies
+    from trex_amd.ragged import RaggedSankoffEngine, RaggedTreePlan
+
+    rng = np.random.default_rng(12)
+    B, Q = 128, 4
+    taxa = rng.integers(8, 65, size=B)
+    Ls = rng.integers(1000, 5001, size=B)
+    chs = [random_topologies(1, int(n), seed=1000 + b)[0] for b, n in enumerate(taxa)]
+    plan = RaggedTreePlan(chs, Ls)
+    leaves = [rng.integers(0, Q, size=(int(n), int(L))).astype(np.int8) for n, L in zip(taxa, Ls)]
+    eng = RaggedSankoffEngine(plan, Q, device)
+    lv = torch.as_tensor(plan.pack_leaves(leaves), device=device)
+    cost = torch.as_tensor((np.ones((Q, Q)) - np.eye(Q)).astype(np.float32), device=device)
+    for _ in range(warmup):
+        eng.value_and_grad(lv, cost, 0.5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.value_and_grad(lv, cost, 0.5)
+    torch.cuda.synchronize()
+    sec = (time.perf_counter() - t0) / steps
+    units = plan.row_sites * Q
+    return {"workload": f"ragged batch: {B} random topologies, 8..64 taxa, 1000..5000 sites, "
+                        f"{Q} states, softmin tau=0.5 fwd+grad in one launch (eager)",
+            "ms_per_step": sec * 1e3, "value": units / sec, "unit": "site-node-state updates/s"}
+
+
 def nk_line(torch, device, steps=50, warmup=5):
     """the NK landscape-aware objective
     (src/trex/evals/benchmark.py:235-306, 586-663) -- one Adam step of
@@ -521,6 +554,8 @@ def main():
             result["c5"] = c5_line(torch, device)
         if not args.no_nk:
             result["nk"] = nk_line(torch, device)
+        if not args.no_ragged:
+            result["ragged"] = ragged_line(torch, device)
     if world > 1 and not args.no_c5:
         result["c5"] = c5_line(torch, device, rank=rank, world=world)
     if rank == 0:

@@ -236,6 +236,39 @@ int trex_adam_step(float* params, const float* grads, float* mu, float* nu, int6
 int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts, void* stream);
 
 /* ========================================================================
+ * Ragged batches: trees of different sizes (n_all_b taxa+ancestors) and
+ * site counts (L_b) in ONE launch -- what trex gets from padding every tree
+ * to MAX_NODES / N buckets with node and site masks (src/trex/padding.py:
+ * 25-27, 77-297) so one jit serves mixed sizes, without the padded work.
+ *   children  int32, tree b's [n_all_b][2] child lists concatenated
+ *   plan      trex_ragged_plan_ints(B, n_all, L) ints; copy to the device
+ *   info      int64 [8] out: n_slots, max_n_leaves, items (64-site work
+ *             items), leaf bytes (sum n_leaves_b L_b), DP row-sites
+ *             (sum n_int_b L_b), sites (sum L_b), backtrack_ok,
+ *             dag | unreached << 32
+ * Packed tensors: leaves int8 [sum n_leaves_b L_b] (tree b: [n_leaves_b][L_b]);
+ * dp / marginals f32 [sum n_int_b L_b][Q] (tree b: [n_int_b][L_b][Q]);
+ * site_score f32 [sum L_b]; anc_states int8 [sum n_int_b L_b];
+ * tree_score / d_tree_score [B].  Q <= 4.  phase: 1 forward, 2 adjoint,
+ * 3 fused (same semantics as trex_sankoff_fwd / _bwd / _fwd_bwd per tree).
+ * ---------------------------------------------------------------------- */
+int64_t trex_ragged_plan_ints(int B, const int32_t* n_all, const int32_t* L);
+int trex_ragged_plan_build(const int32_t* children, const int32_t* n_all, const int32_t* L, int B,
+                           int32_t* plan, int64_t* info);
+int64_t trex_ragged_workspace_bytes(int64_t items, int Q);
+int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_slots, int max_n_leaves,
+                        int64_t items, const int8_t* leaves, const float* cost, int Q, float tau,
+                        unsigned flags, float* dp, float* site_score, float* tree_score,
+                        const float* d_tree_score, float* d_cost, float* marginals,
+                        int8_t* anc_states, void* workspace, int64_t workspace_bytes,
+                        void* stream);
+/* trex-exact ancestral states per tree (backtrack_sankoff_jit) for a ragged
+ * batch; steps = sum n_int_b (plan header int 2). */
+int trex_sankoff_ragged_backtrack(const int32_t* plan, int B, int64_t items, int64_t steps,
+                                  int backtrack_ok, const float* cost, const float* dp, int Q,
+                                  int8_t* anc_states, void* stream);
+
+/* ========================================================================
  * NK landscape-aware loss (src/trex/evals/benchmark.py): the parental
  * guidance term of _compute_loss_landscape_aware_stacked (:235-306) on top
  * of the surrogate cost, with compute_parental_logits (:586-663).

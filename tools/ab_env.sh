@@ -2,7 +2,7 @@
 # A/B the bench under two environment settings on the same box.
 # usage: tools/ab_env.sh "VAR=a" "VAR=b" [reps]   (BENCH_ARGS overrides the bench flags)
 cd "$(dirname "$0")/.."
-ARGS=${BENCH_ARGS:---no-cpu-baseline --no-c5 --no-c2 --no-c3 --no-nk --steps 20}
+ARGS=${BENCH_ARGS:---no-cpu-baseline --no-c5 --no-c2 --no-c3 --no-nk --no-ragged --steps 20}
 for rep in $(seq ${3:-2}); do
   for cfg in "$1" "$2"; do
     env $cfg timeout -k 10 200 python bench.py $ARGS > gpurun_out/ab.json || exit 1

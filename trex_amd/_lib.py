@@ -57,6 +57,14 @@ SIGNATURES = {
     "trex_tree_gram_skip": (_c_i, [_p, _c_i, _c_i64, _c_i, _p, _p, _c_i64, _p]),
     "trex_tree_surrogate_combine": (_c_i, [_p, _p, _c_i, _p, _p, _p, _p, _p]),
     "trex_tree_mf": (_c_i, [_p, _p, _c_i, _c_i64, _p, _p]),
+    # ragged batches
+    "trex_ragged_plan_ints": (_c_i64, [_c_i, _p, _p]),
+    "trex_ragged_plan_build": (_c_i, [_p, _p, _p, _c_i, _p, _p]),
+    "trex_ragged_workspace_bytes": (_c_i64, [_c_i64, _c_i]),
+    "trex_sankoff_ragged": (_c_i, [_c_i, _p, _c_i, _c_i, _c_i, _c_i64, _p, _p, _c_i, _c_f, _c_u,
+                                   _p, _p, _p, _p, _p, _p, _p, _p, _c_i64, _p]),
+    "trex_sankoff_ragged_backtrack": (_c_i, [_p, _c_i, _c_i64, _c_i64, _c_i, _p, _p, _c_i, _p,
+                                             _p]),
     # NK landscape-aware loss
     "trex_nk_parental_logits": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _p, _c_i, _p, _p, _p]),
     "trex_nk_plan_ints": (_c_i64, [_c_i, _c_i, _c_i]),

@@ -300,3 +300,110 @@ extern "C" int trex_plan_build(const int32_t* children, int B, int n_all,
   }
   return TREX_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Ragged batches: trees of different sizes (n_all_b) and site counts (L_b) in
+// one launch.  Layout (ints): header [16] | per-tree records [B][12] |
+// work-item -> tree [items] | forward steps [sum n_int_b][4] |
+// backtrack entries [sum n_int_b][2].  Record: steps offset, n_int, n_leaves,
+// L, first site, first item, leaf byte offset (lo, hi), row-site offset
+// (lo, hi), 2 spare.  One work item = one tree x 64-site tile.
+// ---------------------------------------------------------------------------
+namespace trex {
+namespace {
+constexpr int32_t kRaggedMagic = 0x54525247;  // 'TRRG'
+constexpr int kRaggedMetaInts = 12;           // = kRaggedMeta (sankoff.hip)
+
+bool ragged_shapes(const int32_t* n_all, const int32_t* L, int B, int64_t* steps, int64_t* items) {
+  *steps = 0;
+  *items = 0;
+  for (int b = 0; b < B; ++b) {
+    if (n_all[b] < 3 || n_all[b] > 65535 || L[b] <= 0) return false;
+    *steps += n_all[b] - (n_all[b] + 1) / 2;
+    *items += (L[b] + 63) / 64;
+  }
+  return *items <= 0x7FFFFFFF;
+}
+}  // namespace
+}  // namespace trex
+
+extern "C" int64_t trex_ragged_plan_ints(int B, const int32_t* n_all, const int32_t* L) {
+  if (B <= 0 || !n_all || !L) return 0;
+  int64_t steps, items;
+  if (!trex::ragged_shapes(n_all, L, B, &steps, &items)) return 0;
+  return TREX_PLAN_HEADER_INTS + (int64_t)B * trex::kRaggedMetaInts + items + steps * 6;
+}
+
+extern "C" int trex_ragged_plan_build(const int32_t* children, const int32_t* n_all,
+                                      const int32_t* L, int B, int32_t* plan, int64_t* info) {
+  using namespace trex;
+  int64_t steps, items;
+  if (!children || !n_all || !L || !plan || B <= 0 || !ragged_shapes(n_all, L, B, &steps, &items))
+    return set_error(TREX_E_ARG, "trex_ragged_plan_build: bad arguments (B=%d)", B);
+  int32_t* meta = plan + TREX_PLAN_HEADER_INTS;
+  int32_t* ritem = meta + (int64_t)B * kRaggedMetaInts;
+  int32_t* fwd = ritem + items;
+  int32_t* bt = fwd + steps * 4;
+  std::memset(plan, 0, sizeof(int32_t) * TREX_PLAN_HEADER_INTS);
+  int64_t step_off = 0, item_off = 0, site_off = 0, leaf_off = 0, rows_off = 0, child_off = 0;
+  int max_slots = 0, max_nl = 0, max_ni = 0, all_ok = 1, dag = 0, unr = 0;
+  for (int b = 0; b < B; ++b) {
+    const int na = n_all[b];
+    const int nl = (na + 1) / 2;
+    const int ni = na - nl;
+    int s = 0, ok = 0, d = 0, u = 0;
+    if (!plan_one_tree(children + child_off, na, fwd + step_off * 4, bt + step_off * 2, &s, &ok, &d,
+                       &u))
+      return set_error(TREX_E_TOPOLOGY, "trex_ragged_plan_build: tree %d has an invalid child list",
+                       b);
+    if (site_off > 0x7FFFFFFF)
+      return set_error(TREX_E_UNSUPPORTED, "trex_ragged_plan_build: more than 2^31 sites");
+    if ((int64_t)ni * L[b] * 4 * 4 > 0x7FFFFFF0LL)
+      return set_error(TREX_E_UNSUPPORTED, "trex_ragged_plan_build: tree %d's DP table exceeds 2 GiB",
+                       b);
+    int32_t* m = meta + (int64_t)b * kRaggedMetaInts;
+    m[0] = (int32_t)step_off;
+    m[1] = ni;
+    m[2] = nl;
+    m[3] = L[b];
+    m[4] = (int32_t)site_off;
+    m[5] = (int32_t)item_off;
+    m[6] = (int32_t)(leaf_off & 0xFFFFFFFF);
+    m[7] = (int32_t)(leaf_off >> 32);
+    m[8] = (int32_t)(rows_off & 0xFFFFFFFF);
+    m[9] = (int32_t)(rows_off >> 32);
+    const int tiles = (L[b] + 63) / 64;
+    for (int t = 0; t < tiles; ++t) ritem[item_off + t] = b;
+    max_slots = std::max(max_slots, s);
+    max_nl = std::max(max_nl, nl);
+    max_ni = std::max(max_ni, ni);
+    all_ok &= ok;
+    dag += d;
+    unr += u;
+    step_off += ni;
+    item_off += tiles;
+    site_off += L[b];
+    leaf_off += (int64_t)nl * L[b];
+    rows_off += (int64_t)ni * L[b];
+    child_off += 2LL * na;
+  }
+  plan[0] = kRaggedMagic;
+  plan[1] = B;
+  plan[2] = (int32_t)steps;
+  plan[3] = (int32_t)items;
+  plan[4] = max_slots;
+  plan[5] = max_nl;
+  plan[6] = all_ok;
+  plan[7] = max_ni;
+  if (info) {
+    info[0] = max_slots;  // n_slots for the launch
+    info[1] = max_nl;     // LDS leaf tile rows
+    info[2] = items;      // work items (64-site tiles)
+    info[3] = leaf_off;   // packed leaf bytes: sum n_leaves_b * L_b
+    info[4] = rows_off;   // packed DP row-sites: sum n_int_b * L_b (x Q floats)
+    info[5] = site_off;   // packed sites: sum L_b
+    info[6] = all_ok;     // reference backtrack terminates on every tree
+    info[7] = dag + ((int64_t)unr << 32);
+  }
+  return TREX_OK;
+}

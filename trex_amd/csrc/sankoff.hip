@@ -482,8 +482,17 @@ struct KArgs {
   float* d_cost;        // [Q][Q]
   double* part_tree;    // [B*tiles] per-item score partials
   double* part_dc;      // [Q*Q][B*tiles] per-item dC partials
-  int nblocks;          // B * tiles work items
+  int nblocks;          // B * tiles work items (ragged: sum of per-tree tiles)
+  // ragged batches (null for uniform batches): per-tree records and the
+  // work-item -> tree table of the ragged plan (trex_ragged_plan_build)
+  const int* rmeta;     // [B][kRaggedMeta]
+  const int* ritem;     // [nblocks] tree of each work item
 };
+
+// ragged plan per-tree record (ints): steps offset (in steps), n_int, n_leaves,
+// L, first site (site_score offset), first work item, leaf byte offset (lo, hi),
+// row-site offset of the tree's DP rows (lo, hi; x Q floats), 2 spare
+constexpr int kRaggedMeta = 12;
 
 
 // LDS map (floats): [0, 64) leaf tables: T[code][i] (message; code Q =
@@ -506,8 +515,9 @@ constexpr int kPrefetchRows = 64;  // leaf tiles of <= 64 leaves are prefetched
 // forward, read by the adjoint), so the adjoint reads nothing from HBM; the
 // Sethi-Ullman slots then hold only cotangents.  Costs n_int*Q*256 B of LDS
 // per wave (31 KiB at 32 taxa: one wave per SIMD).
-template <int Q, int SPT, int MODE, int PHASE, bool LFAST, bool RES>
+template <int Q, int SPT, int MODE, int PHASE, bool LFAST, bool RES, bool RAGGED>
 __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
+  static_assert(!RAGGED || (SPT == 1 && !RES), "ragged batches use the SPT=1 re-reading kernels");
   static_assert(!RES || (PHASE == 3 && SPT == 1), "resident mode is the fused SPT=1 kernel");
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
@@ -555,7 +565,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   // only the forward kernel loops over items: the adjoint's register
   // footprint is too large to keep a second tile in flight
   constexpr bool PERSIST = PHASE == 1;
-  const bool pf = PERSIST && SPT == 1 && (L & 3) == 0 && A.nl <= kPrefetchRows;
+  const bool pf = !RAGGED && PERSIST && SPT == 1 && (L & 3) == 0 && A.nl <= kPrefetchRows;
   const int pf_voff = (lane >> 4) * L + (lane & 15) * 4;
   uint32_t pre[kPrefetchRows / 4];
   auto issue_prefetch = [&](int it) {
@@ -578,10 +588,34 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   __syncthreads();  // the table is written by lanes < Q, read by all
 
   do {
-    const int tree = item / A.tiles;
-    const int tile = item - tree * A.tiles;
+    // ---- this item's tree: shape and base offsets ----
+    int tree, tile, n_int, nl, Lt;
+    size_t leaf_base, rows_base, site_base;  // bytes / row-sites / sites
+    cptr<int> prog;
+    if constexpr (RAGGED) {
+      tree = as_const(A.ritem)[item];
+      const cptr<int> m = as_const(A.rmeta) + (size_t)tree * kRaggedMeta;
+      n_int = m[1];
+      nl = m[2];
+      Lt = m[3];
+      site_base = (size_t)(uint32_t)m[4];
+      tile = item - m[5];
+      leaf_base = (size_t)(uint32_t)m[6] | ((size_t)(uint32_t)m[7] << 32);
+      rows_base = (size_t)(uint32_t)m[8] | ((size_t)(uint32_t)m[9] << 32);
+      prog = as_const(reinterpret_cast<const int*>(A.steps)) + (size_t)m[0] * 4;
+    } else {
+      tree = item / A.tiles;
+      tile = item - tree * A.tiles;
+      n_int = A.n_int;
+      nl = A.nl;
+      Lt = L;
+      leaf_base = (size_t)tree * A.nl * L;
+      rows_base = (size_t)tree * A.n_int * L;
+      site_base = (size_t)tree * L;
+      prog = as_const(reinterpret_cast<const int*>(A.steps)) + (size_t)tree * A.n_int * 4;
+    }
     const int site = (tile * kWave + lane) * SPT;
-    const bool active = site < L;
+    const bool active = site < Lt;
     const int sc = active ? site : 0;
 
     // ---- leaf tile of this item ----
@@ -589,26 +623,25 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
       store_prefetch();
       if (item + stride < item_end) issue_prefetch(item + stride);
     } else {
-      const int8_t* lv = A.leaves + (size_t)tree * A.nl * L + sc;
+      const int8_t* lv = A.leaves + leaf_base + sc;
       constexpr int kBatch = 8;
-      for (int c0 = 0; c0 < A.nl; c0 += kBatch) {
+      for (int c0 = 0; c0 < nl; c0 += kBatch) {
         int code[kBatch][SPT];
-        const int nb_ = min(kBatch, A.nl - c0);
+        const int nb_ = min(kBatch, nl - c0);
 #pragma unroll
         for (int u = 0; u < kBatch; ++u)
-          if (u < nb_) ld_codes<SPT>(lv + (size_t)(c0 + u) * L, code[u]);
+          if (u < nb_) ld_codes<SPT>(lv + (size_t)(c0 + u) * Lt, code[u]);
 #pragma unroll
         for (int u = 0; u < kBatch; ++u)
           if (u < nb_) st_codes<SPT>(lleaf + ((c0 + u) * kWave + lane) * SPT, code[u]);
       }
     }
 
-    const cptr<int> prog = as_const(reinterpret_cast<const int*>(A.steps)) + (size_t)tree * A.n_int * 4;
-    const uint32_t treebytes = (uint32_t)((size_t)A.n_int * Q * L * 4);
-    const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * A.n_int * Q * L, treebytes);
+    const uint32_t treebytes = (uint32_t)((size_t)n_int * Q * Lt * 4);
+    const rsrc_t rdp = make_rsrc(A.dp + rows_base * Q, treebytes);
     // inactive lanes address past the buffer: stores drop, loads return 0
     const int voff = active ? site * Q * 4 : 0x7FFFFFF0;
-    const int rowbytes = L * Q * 4;
+    const int rowbytes = Lt * Q * 4;
 
     auto child_code = [&](int desc, int (&code)[SPT]) {
       ld_codes<SPT>(lleaf + ((desc & 0xFFFF) * kWave + lane) * SPT, code);
@@ -620,9 +653,9 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
     if constexpr (FWD) {
       float prev[Q][SPT];  // previous step's D (register bypass, kChildPrev)
       I4 nxt = load_step(prog, 0);
-      for (int k = 0; k < A.n_int; ++k) {
+      for (int k = 0; k < n_int; ++k) {
         const I4 stp = nxt;
-        if (k + 1 < A.n_int) nxt = load_step(prog, k + 1);
+        if (k + 1 < n_int) nxt = load_step(prog, k + 1);
         // gather both children (LDS reads in flight together)
         float d[2][Q][SPT];
 #pragma unroll
@@ -695,7 +728,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
       }
     } else {
       // adjoint only: the root row comes from the table
-      bld_row<Q, SPT>(rdp, voff, (A.n_int - 1) * rowbytes, dv);
+      bld_row<Q, SPT>(rdp, voff, (n_int - 1) * rowbytes, dv);
     }
 
     // ---- root: score + cotangent ----
@@ -706,7 +739,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
       if (active) {
 #pragma unroll
         for (int s = 0; s < SPT; ++s) tot += (double)score[s];
-        if (A.site_score) st<SPT>(A.site_score + (size_t)tree * L + site, score);
+        if (A.site_score) st<SPT>(A.site_score + site_base + site, score);
       }
       tot = wave_sum(tot);
       if (lane == 0) A.part_tree[item] = tot;
@@ -727,9 +760,8 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
         for (int j = 0; j < Q; ++j) acc[i][j] = 0.0f;
       const bool want_marg = A.marg != nullptr;
-      const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * A.n_int * Q * L : A.dp,
-                                   treebytes);
-      int8_t* at = A.anc ? A.anc + (size_t)tree * A.n_int * L + sc : nullptr;
+      const rsrc_t rmg = make_rsrc(want_marg ? A.marg + rows_base * Q : A.dp, treebytes);
+      int8_t* at = A.anc ? A.anc + rows_base + sc : nullptr;
       lds_put<Q, SPT>(slots, kRootSlot, lane, groot);
 
       // DP rows of a step's internal children are loaded one step ahead into
@@ -776,7 +808,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
               if (g[i][s] > bv) { bv = g[i][s]; bi = i; }
             best[s] = bi;
           }
-          st_codes<SPT>(at + (size_t)row * L, best);
+          st_codes<SPT>(at + (size_t)row * Lt, best);
         }
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -846,8 +878,8 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
       if constexpr (RES) {
         // D of the internal children from the resident table; the next
         // step's program words are loaded one step ahead
-        I4 sn = load_step(prog, A.n_int - 1);
-        for (int k = A.n_int - 1; k >= 0; --k) {
+        I4 sn = load_step(prog, n_int - 1);
+        for (int k = n_int - 1; k >= 0; --k) {
           const I4 cur = sn;
           if (k >= 1) sn = load_step(prog, k - 1);
           float cd[2][Q][SPT];
@@ -860,11 +892,11 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         }
       } else {
       float bufA[2][Q][SPT], bufB[2][Q][SPT];
-      I4 sA = load_step(prog, A.n_int - 1);
-      I4 sB = A.n_int > 1 ? load_step(prog, A.n_int - 2) : sA;
+      I4 sA = load_step(prog, n_int - 1);
+      I4 sB = n_int > 1 ? load_step(prog, n_int - 2) : sA;
       const I4 none = {0, 0, 0, 0};  // sentinel children only: prefetch reads nothing
       prefetch(sA, bufA);
-      for (int k = A.n_int - 1; k >= 0; k -= 2) {
+      for (int k = n_int - 1; k >= 0; k -= 2) {
         // step k uses A while B fills for step k-1
         prefetch(k >= 1 ? sB : none, bufB);
         const I4 cA = sA;
@@ -894,7 +926,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   } while (PERSIST && item < item_end);
 }
 
-template <int Q, int SPT, int MODE, int PHASE, bool RES = false>
+template <int Q, int SPT, int MODE, int PHASE, bool RES = false, bool RAGGED = false>
 __device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds) {
   // leaf messages have the closed form C[i][code] when the 1e5 sentinel
   // dominates (hard: range(C) < 1e5; soft: exp(-(1e5 - range)/tau) < 2^-64)
@@ -903,24 +935,24 @@ __device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds
   const float range = cmax - cmin;
   const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
   if (lfast)
-    sankoff_body<Q, SPT, MODE, PHASE, true, RES>(A, lds);
+    sankoff_body<Q, SPT, MODE, PHASE, true, RES, RAGGED>(A, lds);
   else
-    sankoff_body<Q, SPT, MODE, PHASE, false, RES>(A, lds);
+    sankoff_body<Q, SPT, MODE, PHASE, false, RES, RAGGED>(A, lds);
 }
 
-template <int Q, int SPT, bool SOFT, int PHASE>
+template <int Q, int SPT, bool SOFT, int PHASE, bool RAGGED = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? 6 : 5, 8)))
 void sankoff_kernel(KArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if constexpr (!SOFT) {
-    sankoff_dispatch_leaf<Q, SPT, kHard, PHASE>(A, lds);
+    sankoff_dispatch_leaf<Q, SPT, kHard, PHASE, false, RAGGED>(A, lds);
   } else {
     float cmin, cmax;
     cost_range<Q>(A.cost, cmin, cmax);
     if (use_ktrick(cmin, cmax, A.a))
-      sankoff_dispatch_leaf<Q, SPT, kSoftK, PHASE>(A, lds);
+      sankoff_dispatch_leaf<Q, SPT, kSoftK, PHASE, false, RAGGED>(A, lds);
     else
-      sankoff_dispatch_leaf<Q, SPT, kSoftDirect, PHASE>(A, lds);
+      sankoff_dispatch_leaf<Q, SPT, kSoftDirect, PHASE, false, RAGGED>(A, lds);
   }
 }
 
@@ -945,12 +977,30 @@ void sankoff_res_kernel(KArgs A) {
 // --------------------------------------------------------------------------
 // trex-exact ancestral reconstruction (sankoff.py:166-185, 191-267)
 // --------------------------------------------------------------------------
-template <int Q, int SPT>
+// RAGGED: bt points at the ragged plan's records (rmeta), the item table
+// follows them, then the steps and the backtrack entries (see plan.cpp)
+template <int Q, int SPT, bool RAGGED = false>
 __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
     const int2* __restrict__ bt, const float* __restrict__ cost, const float* __restrict__ dp,
-    int n_int, int L, int tiles, int8_t* __restrict__ anc) {
-  const int tree = blockIdx.x / tiles;
-  const int tile = blockIdx.x - tree * tiles;
+    int n_int, int L, int tiles, int8_t* __restrict__ anc, const int* __restrict__ rmeta = nullptr,
+    int B = 0, int items = 0, int steps = 0) {
+  int tree, tile;
+  size_t rows_base;
+  if constexpr (RAGGED) {
+    const int item = blockIdx.x;
+    tree = as_const(rmeta + (size_t)B * kRaggedMeta)[item];
+    const cptr<int> m = as_const(rmeta) + (size_t)tree * kRaggedMeta;
+    n_int = m[1];
+    L = m[3];
+    tile = item - m[5];
+    rows_base = (size_t)(uint32_t)m[8] | ((size_t)(uint32_t)m[9] << 32);
+    bt = reinterpret_cast<const int2*>(rmeta + (size_t)B * kRaggedMeta + items + (size_t)steps * 4) +
+         m[0];
+  } else {
+    tree = blockIdx.x / tiles;
+    tile = blockIdx.x - tree * tiles;
+    rows_base = (size_t)tree * n_int * L;
+  }
   const int lane = threadIdx.x;
   const int site = (tile * kWave + lane) * SPT;
   if (site >= L) return;
@@ -959,10 +1009,10 @@ __global__ __launch_bounds__(kWave) void sankoff_backtrack_kernel(
   for (int i = 0; i < Q; ++i)
 #pragma unroll
     for (int j = 0; j < Q; ++j) c[i][j] = as_const(cost)[i * Q + j];
-  const cptr<int> prog = as_const(reinterpret_cast<const int*>(bt)) + (size_t)tree * n_int * 2;
+  const cptr<int> prog = as_const(reinterpret_cast<const int*>(bt)) + (RAGGED ? 0 : (size_t)tree * n_int * 2);
   const size_t rowstride = (size_t)Q * L;  // site-major rows [L][Q]
-  const float* dpt = dp + (size_t)tree * n_int * rowstride + (size_t)site * Q;
-  int8_t* at = anc + (size_t)tree * n_int * L + site;
+  const float* dpt = dp + rows_base * Q + (size_t)site * Q;
+  int8_t* at = anc + rows_base + site;
   for (int k = 0; k < n_int; ++k) {
     const int2 e = make_int2(prog[2 * k], prog[2 * k + 1]);
     const int x = e.x & 0xFFFF;
@@ -1290,6 +1340,8 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   if (lds > (res ? kLdsPerCu : 65536)) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
   if ((int64_t)B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
   KArgs A;
+  A.rmeta = nullptr;
+  A.ritem = nullptr;
   A.steps = reinterpret_cast<const int4*>(plan + TREX_PLAN_HEADER_INTS);
   A.leaves = leaves;
   A.cost = cost;
@@ -1330,6 +1382,20 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   }
   if (int e = hip_check(fn)) return e;
   return partial_reduce(fn, A.part_tree, A.part_dc, B, tiles, Q, phase, tree_score, d_cost, stream);
+}
+
+template <int Q, bool SOFT>
+void launch_ragged(int phase, size_t lds, hipStream_t st, const KArgs& A) {
+  auto go = [&](auto kernel) {
+    const int grid = phase == 1 ? persistent_grid(kernel, lds, A.nblocks) : (A.nblocks + 7) / 8 * 8;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kWave), lds, st, A);
+  };
+  if (phase == 1)
+    go(sankoff_kernel<Q, 1, SOFT, 1, true>);
+  else if (phase == 2)
+    go(sankoff_kernel<Q, 1, SOFT, 2, true>);
+  else
+    go(sankoff_kernel<Q, 1, SOFT, 3, true>);
 }
 
 }  // namespace
@@ -1438,4 +1504,103 @@ extern "C" int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int
   hipLaunchKernelGGL(to_trex_layout_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, dp,
                      leaves, B, L, n_all, nl, Q, out);
   return hip_check("trex_dp_to_trex_layout");
+}
+
+// ---------------------------------------------------------------------------
+// Ragged batches (trees of different n_all / L in one launch; plan from
+// trex_ragged_plan_build).  Packed layouts: leaves [sum n_leaves_b * L_b]
+// int8 (tree b at its leaf offset, [n_leaves_b][L_b]); dp / marginals
+// [sum n_int_b * L_b][Q] f32 (tree b: [n_int_b][L_b][Q]); site_score
+// [sum L_b]; anc_states [sum n_int_b * L_b] int8.
+// ---------------------------------------------------------------------------
+extern "C" int64_t trex_ragged_workspace_bytes(int64_t items, int Q) {
+  if (items <= 0 || Q <= 0) return 0;
+  return items * 8 * (1 + (int64_t)Q * Q) + 256;
+}
+
+extern "C" int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_slots, int max_nl,
+                                   int64_t items, const int8_t* leaves, const float* cost, int Q,
+                                   float tau, unsigned flags, float* dp, float* site_score,
+                                   float* tree_score, const float* d_tree_score, float* d_cost,
+                                   float* marginals, int8_t* anc_states, void* workspace,
+                                   int64_t workspace_bytes, void* stream) {
+  const char* fn = "trex_sankoff_ragged";
+  if (phase < 1 || phase > 3) return set_error(TREX_E_ARG, "%s: phase must be 1, 2 or 3", fn);
+  if (B <= 0 || items <= 0 || items > 0x7FFFFFFF || max_nl < 2 || Q < 2)
+    return set_error(TREX_E_ARG, "%s: bad shape B=%d items=%lld max_nl=%d Q=%d", fn, B,
+                     (long long)items, max_nl, Q);
+  if (Q > 4) return set_error(TREX_E_UNSUPPORTED, "%s: ragged batches support Q <= 4", fn);
+  if (!plan || !leaves || !cost || !workspace || !dp)
+    return set_error(TREX_E_ARG, "%s: null pointer argument", fn);
+  if ((phase & 1) && !tree_score) return set_error(TREX_E_ARG, "%s: tree_score is required", fn);
+  if ((phase & 2) && !d_cost) return set_error(TREX_E_ARG, "%s: d_cost is required", fn);
+  if (!(tau >= 0.0f) || std::isinf(tau))
+    return set_error(TREX_E_ARG, "%s: tau must be finite and >= 0 (got %g)", fn, tau);
+  if (workspace_bytes < trex_ragged_workspace_bytes(items, Q))
+    return set_error(TREX_E_ARG, "%s: workspace too small", fn);
+  if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  const size_t lds = lds_bytes(n_slots, max_nl, Q, 1);
+  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
+  KArgs A;
+  const int* meta = plan + TREX_PLAN_HEADER_INTS;
+  A.rmeta = meta;
+  A.ritem = meta + (size_t)B * kRaggedMeta;
+  A.steps = reinterpret_cast<const int4*>(A.ritem + items);
+  A.leaves = leaves;
+  A.cost = cost;
+  A.n_int = 0;
+  A.nl = max_nl;
+  A.L = 0;
+  A.tiles = 0;
+  A.B = B;
+  A.n_slots = n_slots;
+  tau_coefs(tau, &A.a, &A.bcoef);
+  A.hard_root = (flags & TREX_FLAG_HARD_ROOT) ? 1 : 0;
+  A.dp = dp;
+  A.site_score = site_score;
+  A.tree_score = tree_score;
+  A.dts = d_tree_score;
+  A.marg = marginals;
+  A.anc = anc_states;
+  A.d_cost = d_cost;
+  A.nblocks = (int)items;
+  A.part_tree = reinterpret_cast<double*>(workspace);
+  A.part_dc = A.part_tree + items;
+  const bool soft = tau > 0.0f;
+  hipStream_t st = (hipStream_t)stream;
+  switch (Q) {
+    case 2: soft ? launch_ragged<2, true>(phase, lds, st, A) : launch_ragged<2, false>(phase, lds, st, A); break;
+    case 3: soft ? launch_ragged<3, true>(phase, lds, st, A) : launch_ragged<3, false>(phase, lds, st, A); break;
+    case 4: soft ? launch_ragged<4, true>(phase, lds, st, A) : launch_ragged<4, false>(phase, lds, st, A); break;
+  }
+  if (int e = hip_check(fn)) return e;
+  return partial_reduce(fn, A.part_tree, A.part_dc, B, 0, Q, phase, tree_score, d_cost, stream,
+                        meta + 5, kRaggedMeta, (int)items);
+}
+
+extern "C" int trex_sankoff_ragged_backtrack(const int32_t* plan, int B, int64_t items,
+                                             int64_t steps, int backtrack_ok, const float* cost,
+                                             const float* dp, int Q, int8_t* anc_states,
+                                             void* stream) {
+  const char* fn = "trex_sankoff_ragged_backtrack";
+  if (B <= 0 || items <= 0 || items > 0x7FFFFFFF || steps <= 0 || Q < 2)
+    return set_error(TREX_E_ARG, "%s: bad arguments", fn);
+  if (Q > 4) return set_error(TREX_E_UNSUPPORTED, "%s: ragged batches support Q <= 4", fn);
+  if (!backtrack_ok)
+    return set_error(TREX_E_TOPOLOGY,
+                     "%s: the reference backtrack does not terminate on this batch (cyclic child "
+                     "references)", fn);
+  if (!plan || !cost || !dp || !anc_states) return set_error(TREX_E_ARG, "%s: null pointer", fn);
+  const int* meta = plan + TREX_PLAN_HEADER_INTS;
+  hipStream_t st = (hipStream_t)stream;
+#define TREX_RBT(QQ)                                                                          \
+  hipLaunchKernelGGL((sankoff_backtrack_kernel<QQ, 1, true>), dim3((int)items), dim3(kWave), 0, \
+                     st, nullptr, cost, dp, 0, 0, 0, anc_states, meta, B, (int)items, (int)steps);
+  switch (Q) {
+    case 2: TREX_RBT(2) break;
+    case 3: TREX_RBT(3) break;
+    case 4: TREX_RBT(4) break;
+  }
+#undef TREX_RBT
+  return hip_check(fn);
 }

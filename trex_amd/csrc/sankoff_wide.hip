@@ -478,19 +478,28 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
                                                           const double* __restrict__ part_dc,
                                                           int B, int tiles, int Q2, int do_tree,
                                                           float* __restrict__ tree_score,
-                                                          float* __restrict__ d_cost) {
+                                                          float* __restrict__ d_cost,
+                                                          const int* __restrict__ first,
+                                                          int first_stride, int items) {
   __shared__ double red[256];
   const int b = blockIdx.x;
   const double* src;
   int n;
   float* dst;
   if (do_tree && b < B) {
-    src = part_tree + (size_t)b * tiles;
-    n = tiles;
+    if (first) {  // ragged: tree b owns items [first[b], first[b + 1])
+      const int lo = first[(size_t)b * first_stride];
+      const int hi = b + 1 < B ? first[(size_t)(b + 1) * first_stride] : items;
+      src = part_tree + lo;
+      n = hi - lo;
+    } else {
+      src = part_tree + (size_t)b * tiles;
+      n = tiles;
+    }
     dst = tree_score + b;
   } else {
     const int q = b - (do_tree ? B : 0);
-    const size_t nb = (size_t)B * tiles;
+    const size_t nb = first ? (size_t)items : (size_t)B * tiles;
     src = part_dc + (size_t)q * nb;
     n = (int)nb;
     dst = d_cost + q;
@@ -647,12 +656,14 @@ int wide_run(const char* fn, const WideCall& c) {
 }
 
 int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
-                   int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream) {
+                   int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream,
+                   const int* first, int first_stride, int items) {
   const bool do_tree = (phase & 1) != 0;
   const bool do_dc = (phase & 2) != 0;
   const int rgrid = (do_tree ? B : 0) + (do_dc ? Q * Q : 0);
   hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(256), 0, (hipStream_t)stream,
-                     part_tree, part_dc, B, tiles, Q * Q, do_tree ? 1 : 0, tree_score, d_cost);
+                     part_tree, part_dc, B, tiles, Q * Q, do_tree ? 1 : 0, tree_score, d_cost,
+                     first, first_stride, items);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
   return TREX_OK;

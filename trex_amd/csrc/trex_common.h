@@ -59,8 +59,11 @@ int64_t wide_workspace_bytes(int B, int L, int Q);
 int wide_run(const char* fn, const WideCall& c);
 // fixed-order sum of per-item partials -> tree_score [B] (phase & 1), d_cost
 // [Q*Q] (phase & 2); part_dc is [Q*Q][B*tiles]
+// (ragged batches: first[b * first_stride] is tree b's first item, items the
+// total; tiles is then unused)
 int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
-                   int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream);
+                   int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream,
+                   const int* first = nullptr, int first_stride = 0, int items = 0);
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream);
 
