@@ -1,0 +1,156 @@
+"""Synthetic data generators of trex, restated on the host (numpy).
+
+SURVEY.md §8(f) rank 3: the ground-truth and NK-model generators feed the
+benchmarks; they are not on the hot path, and the survey's plan is that host
+numpy suffices.  Restated processes (values differ: the reference draws with
+JAX's threefry PRNG, which cannot run here; ``seed`` seeds numpy's PCG64):
+
+* ``mutate``               src/trex/ground_truth.py:20-52
+* ``generate_groundtruth`` src/trex/ground_truth.py:112-197
+* ``create_nk_model_landscape`` src/trex/nk_model.py:17-43
+* ``get_fitness``          src/trex/nk_model.py:46-110
+* ``generate_tree_data``   src/trex/nk_model.py:116-278, including its index
+  semantics: the root is the first node whose argmax parent is itself
+  (``jnp.where(..., size=1)`` fills 0 when there is none), BFS order from it,
+  and unfilled BFS slots are -1, which index the LAST node (numpy/JAX
+  negative-index wrap), as in the reference.
+
+Outputs are numpy arrays in the reference's dtypes/shapes; move them to the
+device with torch when a kernel needs them.
+"""
+
+from __future__ import annotations
+
+from collections import namedtuple
+
+import numpy as np
+
+PhylogeneticTree = namedtuple("PhylogeneticTree",
+                              ["masked_sequences", "all_sequences", "adjacency"])
+
+
+def _rng(seed):
+    return seed if isinstance(seed, np.random.Generator) else np.random.default_rng(seed)
+
+
+def mutate(rng, sequence, n_states: int, n_mutations: int) -> np.ndarray:
+    """Exactly ``n_mutations`` distinct sites get (x + U{1..Q-1}) mod Q
+    (ground_truth.py:39-52).  int8."""
+    rng = _rng(rng)
+    seq = np.asarray(sequence)
+    mask = np.zeros(seq.shape[0], dtype=bool)
+    if n_mutations > 0:
+        mask[rng.choice(seq.shape[0], size=n_mutations, replace=False)] = True
+    offsets = rng.integers(1, n_states, size=seq.shape)
+    return np.where(mask, (seq + offsets) % n_states, seq).astype(np.int8)
+
+
+def generate_groundtruth(n_leaves: int, n_states: int, n_mutations: int, seq_length: int,
+                         seed: int = 42) -> PhylogeneticTree:
+    """Balanced tree from a zero root, children = mutate(parent) per split
+    (ground_truth.py:112-197).  float32 outputs as the reference."""
+    if not (n_leaves > 0 and (n_leaves & (n_leaves - 1)) == 0):
+        raise ValueError("n_leaves must be a power of 2.")
+    rng = _rng(seed)
+    n_anc = n_leaves - 1
+    n_all = n_leaves + n_anc
+    seqs = np.zeros((n_all, seq_length), dtype=np.int8)
+    for i in range(n_anc):  # parents from the root down (:165-178)
+        parent = n_all - 1 - i
+        p_i = parent - n_leaves
+        seqs[2 * p_i] = mutate(rng, seqs[parent], n_states, n_mutations)
+        seqs[2 * p_i + 1] = mutate(rng, seqs[parent], n_states, n_mutations)
+    masked = np.zeros_like(seqs)
+    masked[:n_leaves] = seqs[:n_leaves]
+    adj = np.zeros((n_all, n_all), dtype=np.float32)
+    i = np.arange(n_anc)
+    adj[2 * i, n_leaves + i] = 1
+    adj[2 * i + 1, n_leaves + i] = 1
+    return PhylogeneticTree(masked.astype(np.float32), seqs.astype(np.float32), adj)
+
+
+def create_nk_model_landscape(n: int, k: int, seed=0, n_states: int = 2) -> dict:
+    """interactions U{0..n-1} (n, k), fitness tables U[0, 1) (n, q^(k+1))
+    (nk_model.py:31-43)."""
+    rng = _rng(seed)
+    return {"interactions": rng.integers(0, n, size=(n, k)).astype(np.int32),
+            "fitness_tables": rng.uniform(size=(n, n_states ** (k + 1))).astype(np.float32),
+            "n_states": n_states, "k": k}
+
+
+def get_fitness(sequence, landscape: dict, seq_mask=None) -> float:
+    """Masked mean of f_i at index sum_j s_j q^j with s_0 the site's own
+    state (nk_model.py:89-110; least-significant-first, unlike the parental
+    logits' table reshape)."""
+    seq = np.asarray(sequence).astype(np.int64).reshape(-1)
+    inter = np.asarray(landscape["interactions"])
+    q = int(landscape["n_states"])
+    n = seq.shape[0]
+    mask = np.ones(n, bool) if seq_mask is None else np.asarray(seq_mask, bool)
+    idx = np.concatenate([np.arange(n)[:, None], inter], axis=1)
+    powers = q ** np.arange(idx.shape[1])
+    table_idx = (seq[idx] * powers).sum(1)
+    vals = np.asarray(landscape["fitness_tables"])[np.arange(n), table_idx]
+    return float((vals * mask).sum() / mask.sum())
+
+
+def _bfs_order(adjacency, parent):
+    n = adjacency.shape[0]
+    selfp = np.nonzero(parent == np.arange(n))[0]
+    root = int(selfp[0]) if selfp.size else 0  # jnp.where(size=1) fill value 0
+    order = np.full(n, -1, dtype=np.int64)
+    visited = np.zeros(n, bool)
+    queue = [root]
+    t = 0
+    while queue:
+        node = queue.pop(0)
+        order[int(visited.sum())] = node
+        visited[node] = True
+        for c in np.nonzero(adjacency[:, node] == 1)[0]:
+            if not visited[c]:
+                queue.append(int(c))
+        t += 1
+        if t > n:
+            break
+    return root, order
+
+
+def generate_tree_data(landscape: dict, adjacency, root_sequence, mutation_rate: float, seed=0,
+                       coupled_mutation_prob: float = 0.5, n_states: int = 20,
+                       mutation_rate_noise_std: float = 0.0,
+                       branch_length: int = 1) -> PhylogeneticTree:
+    """NK-model sequence evolution along a tree with Metropolis acceptance
+    (nk_model.py:116-278)."""
+    rng = _rng(seed)
+    A = np.asarray(adjacency)
+    n = A.shape[0]
+    root_seq = np.asarray(root_sequence).reshape(-1)
+    L = root_seq.shape[0]
+    if "n_states" in landscape:
+        n_states = int(landscape["n_states"])
+    parent = np.argmax(A, axis=1)
+    root, order = _bfs_order(A, parent)
+    seqs = np.zeros((n, L), dtype=np.int64)
+    seqs[root] = root_seq
+    inter = np.asarray(landscape["interactions"])
+    for i in range(n):
+        node = int(order[i])  # -1 wraps to the last node, as in the reference
+        if node == root:
+            continue
+        rate = min(mutation_rate * np.exp(rng.normal() * mutation_rate_noise_std), 1.0)
+        seq = seqs[parent[node]].copy()
+        for _ in range(branch_length):
+            if rng.random() < coupled_mutation_prob:
+                site = int(rng.integers(0, L))
+                mask = np.zeros(L, bool)
+                mask[np.concatenate([[site], inter[site]]).astype(np.int64)] = True
+                proposal = np.where(mask, rng.integers(0, n_states, size=L), seq)
+            else:
+                mask = rng.random(L) < rate
+                proposal = np.where(mask, rng.integers(0, n_states, size=L), seq)
+            acc = np.exp(get_fitness(proposal, landscape) - get_fitness(seq, landscape))
+            if rng.random() < min(1.0, acc):
+                seq = proposal
+        seqs[node] = seq
+    return PhylogeneticTree(np.zeros((n, L), np.float32), seqs.astype(np.float32),
+                            A.astype(np.float32))
