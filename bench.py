@@ -253,16 +253,14 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
     sites shard: one all-reduce of the 511 x 511 Gram per step
     (strong scaling: the 50 000 sites are split).  Eager launches (Adam's bias
     correction changes every step)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from _cases import simulate_leaves
-
+    from trex_amd.datagen import generate_groundtruth
     from trex_amd.distributed import shard_bounds
     from trex_amd.tree import TreeOptimizer, gumbel_noise
 
     nl, L, Q = 256, 50000, 4
     n = 2 * nl - 1
     lo, hi = shard_bounds(L, rank, world)
-    seqs, _ = simulate_leaves(nl, L, Q, 5, seed=6)
+    seqs = generate_groundtruth(nl, Q, 5, L, seed=6).all_sequences.astype(np.int8)
     S = torch.zeros((n, hi - lo, Q), dtype=torch.float32, device=device)
     S[:nl] = torch.nn.functional.one_hot(
         torch.as_tensor(seqs[:nl, lo:hi].astype(np.int64), device=device), Q).float()
@@ -343,8 +341,8 @@ def nk_line(torch, device, steps=50, warmup=5):
     run_trex_landscape_aware_configurable (loss + grad + optax adam), at the
     reference's eval shape (benchmark.py:981-985: 32 leaves, N = 15 sites,
     binary states, K = 10, lambda = 3) and at a larger DNA shape."""
-    from oracle.nk_ref import random_landscape  # synthetic landscape (shapes only)
     from trex_amd import nk as NK
+    from trex_amd.datagen import create_nk_model_landscape
     from trex_amd.tree import Adam
 
     out = {}
@@ -352,7 +350,8 @@ def nk_line(torch, device, steps=50, warmup=5):
                                      "dna_256x2000_q4_k4": (256, 2000, 4, 4, 1.0)}.items():
         n_all = 2 * nl - 1
         rng = np.random.default_rng(8)
-        inter, F = random_landscape(L, k, Q, seed=9)
+        land_np = create_nk_model_landscape(L, k, seed=9, n_states=Q)
+        inter, F = land_np["interactions"], land_np["fitness_tables"]
         A = np.zeros((n_all, n_all), np.float32)
         A[np.arange(n_all - 1), nl + np.arange(n_all - 1) // 2] = 1.0
         land = NK.NKLandscape(inter, F, Q, device)
