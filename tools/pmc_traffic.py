@@ -28,8 +28,8 @@ def counters(d):
 
 
 def short(name):
-    m = re.search(r"(sankoff_kernel|rows_load|stream_load|rows_kernel|stream_kernel|wide_reduce_kernel)"
-                  r"(<[^>(]*>)?", name)
+    m = re.search(r"(sankoff_kernel|rows_load|stream_load|rows_kernel|stream_kernel|"
+                  r"sitemajor_kernel|wide_reduce_kernel)(<[^>(]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name[:50]
 
 
@@ -45,19 +45,28 @@ def main():
     fetch_rows = cal["rows_load"]["FETCH_SIZE"] * 1024
     fetch_stream = cal["stream_load"]["FETCH_SIZE"] * 1024
     write_rows = cal["rows_kernel<1>"]["WRITE_SIZE"] * 1024 if "rows_kernel<1>" in cal else None
+    write_sm = cal["sitemajor_kernel"]["WRITE_SIZE"] * 1024 if "sitemajor_kernel" in cal else None
     corr = {"fetch_4B_rows": known / fetch_rows, "fetch_16B_stream": known / fetch_stream,
-            "write_4B_rows": (known / write_rows) if write_rows else 1.0}
+            "write_4B_rows": (known / write_rows) if write_rows else 1.0,
+            "write_16B_sitemajor": (known / write_sm) if write_sm else 1.0}
+    # the site-major DP table (trex_version >= 4) is read and written 16 B per
+    # lane: the 16-B stream / site-major store corrections apply
+    fetch_corr = corr["fetch_16B_stream"]
+    write_corr = corr["write_16B_sitemajor"] if write_sm else corr["write_4B_rows"]
     res = {"workload_key": a.workload_key, "calibration": corr, "kernels": {}}
     for k, v in counters(a.pmc).items():
         s = short(k)
         if "sankoff_kernel" not in s:
             continue
-        f = v.get("FETCH_SIZE", 0.0) * 1024 * corr["fetch_4B_rows"]
-        w = v.get("WRITE_SIZE", 0.0) * 1024 * corr["write_4B_rows"]
+        f = v.get("FETCH_SIZE", 0.0) * 1024 * fetch_corr
+        w = v.get("WRITE_SIZE", 0.0) * 1024 * write_corr
         res["kernels"][s] = {"fetch_bytes": f, "write_bytes": w, "traffic_bytes": f + w}
-    # phase -> bench kernel name (sankoff_kernel<Q, SPT, SOFT, PHASE>)
+    # phase -> bench kernel name (sankoff_kernel<Q, SPT, SOFT, PHASE, RAGGED>)
     for s, e in res["kernels"].items():
-        ph = s.rstrip(">").split(",")[-1].strip()
+        args = [x.strip() for x in s.split("<", 1)[1].rstrip(">").split(",")]
+        if len(args) > 4 and args[4] == "true":
+            continue  # ragged instantiation
+        ph = args[3]
         name = {"1": "sankoff_fwd", "2": "sankoff_bwd", "3": "sankoff_fwd_bwd"}.get(ph)
         if name:
             res[name] = e["traffic_bytes"]
