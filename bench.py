@@ -294,13 +294,16 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
     # build executes less (symmetric Gram tiles; dS for ancestor rows only),
     # so this is a trex-equivalent rate, not the MFMA utilisation.
     flops = 4.0 * n * n * L * Q
+    gemm_desc = ("f16x3 split-product MFMA GEMMs (f32 accumulate; held to rtol 1e-5 vs fp64 "
+                 "like the f32 path)" if opt.gemm == "x3" else "f32 MFMA GEMMs")
     return {"workload": "C5: 511-node relaxed tree x 50000 sites x 4 states, joint Adam step "
-                        "(surrogate + constraint + VJPs + optax adam), f32 MFMA GEMMs"
+                        "(surrogate + constraint + VJPs + optax adam), " + gemm_desc
                         + (f"; sites sharded over {world} ranks, Gram all-reduce" if world > 1
                            else ""),
             "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec, "n_gpus": world,
             "scaling": "strong" if world > 1 else None,
-            "trex_equivalent_gemm_tflops": flops / sec / 1e12, "loss_last": float(loss)}
+            "trex_equivalent_gemm_tflops": flops / sec / 1e12, "loss_last": float(loss),
+            "gemm": opt.gemm}
 
 
 def ragged_line(torch, device, steps=20, warmup=3):

@@ -209,6 +209,18 @@ int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS, vo
  * tree.py:127), which halves the MF GEMM at N = 2 n_leaf - 1. */
 int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t K, int row0, int nrows,
                       float* dS_rows, void* stream);
+/* f16x3 split-product versions of trex_tree_gram_skip / trex_tree_mf_rows:
+ * each operand x is scaled by a power of two and split into f16 hi + lo
+ * (22 significant bits), products hi*hi + hi*lo + lo*hi on f16 MFMA with f32
+ * accumulation -- ~5x fewer MFMA cycles than the f32 MFMA, accuracy within
+ * the same 1e-5 relative bar vs fp64 (tests/test_tree_gpu.py).  Contract:
+ * every |operand| <= its max_abs (the optimisation loop's S is a softmax /
+ * one-hot, max 1; M = diag(r+c) - (A+A^T) with softmax rows of A, max N+1);
+ * a larger value overflows f16 (inf).  K % 16 == 0 for the Gram. */
+int trex_tree_gram_skip_x3(const float* S, int N, int64_t K, int skip_rows, float max_abs,
+                           float* G, void* workspace, int64_t workspace_bytes, void* stream);
+int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64_t K, int row0, int nrows,
+                         float max_abs_m, float max_abs_s, float* dS_rows, void* stream);
 
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */

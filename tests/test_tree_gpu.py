@@ -189,11 +189,14 @@ def test_c5_scale_gram_properties(device):
     assert float(dA1[i, j]) == L - agree
 
 
-def test_tree_optimizer_matches_oracle_loop(device):
-    """The fused device loop == oracle compute_loss + adam, step by step."""
-    params, noise, seqs = _tree_case(16, 50, 4, 17)
+@pytest.mark.parametrize("gemm", ["x3", "f32"])
+def test_tree_optimizer_matches_oracle_loop(device, gemm):
+    """The fused device loop == oracle compute_loss + adam, step by step
+    (both GEMM precisions: f16x3 split products and f32 MFMA)."""
+    params, noise, seqs = _tree_case(16, 52, 4, 17)  # K = 208, a multiple of 16
     opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
-                          lr=0.01)
+                          lr=0.01, gemm=gemm)
+    assert opt.gemm == gemm
     p_ref = {k: v.astype(np.float64) for k, v in params.items()}
     st = T.adam_init(p_ref)
     nz = _t(noise, device)
@@ -247,3 +250,40 @@ def test_gram_skip_keeps_cached_block(device):
     mask = torch.ones((N, N), dtype=torch.bool, device=device)
     mask[:t0, :t0] = False
     assert torch.equal(G[mask], full[mask])
+
+
+@pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (100, 1024, 0), (64, 16, 0)])
+def test_split_gram_and_mf_vs_fp64(device, N, K, skip):
+    """f16x3 split-product Gram / MF (trex_tree_gram_skip_x3 /
+    trex_tree_mf_rows_x3) vs fp64 at the f32 path's bar: softmax-like S
+    (values spanning 1e-6 .. 1, one-hot rows) and M = diag(r+c) - (A+A^T)
+    with softmax rows of A."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    rng = np.random.default_rng(N + K)
+    logits = rng.normal(scale=3.0, size=(N, K // 4, 4))
+    P = np.exp(logits - logits.max(-1, keepdims=True))
+    P /= P.sum(-1, keepdims=True)
+    P[: N // 3] = np.eye(4)[rng.integers(0, 4, size=(N // 3, K // 4))]  # one-hot leaf rows
+    S = P.reshape(N, K).astype(np.float32)
+    Al = rng.normal(size=(N, N))
+    A = np.exp(Al - Al.max(1, keepdims=True))
+    A /= A.sum(1, keepdims=True)
+    M = (np.diag(A.sum(1) + A.sum(0)) - (A + A.T)).astype(np.float32)
+    St, Mt = _t(S, device), _t(M, device)
+    ws = torch.empty(int(lib().trex_tree_workspace_bytes(N, K)), dtype=torch.uint8, device=device)
+    st = stream_handle(torch.device(device))
+    Gx = torch.zeros((N, N), device=device)
+    check(lib().trex_tree_gram_skip_x3(ptr(St), N, K, skip, 1.0, ptr(Gx), ptr(ws), ws.numel(), st))
+    S64 = S.astype(np.float64)
+    Gref = S64 @ S64.T
+    t0 = (skip // 64) * 64
+    mask = np.ones((N, N), bool)
+    mask[:t0, :t0] = False
+    np.testing.assert_allclose(_n(Gx)[mask], Gref[mask], rtol=1e-5, atol=1e-5 * Gref.max())
+    r0 = N // 2
+    out = torch.empty((N - r0, K), device=device)
+    check(lib().trex_tree_mf_rows_x3(ptr(Mt), ptr(St), N, K, r0, N - r0, float(N + 1), 1.0,
+                                     ptr(out), st))
+    ref = M.astype(np.float64)[r0:] @ S64
+    np.testing.assert_allclose(_n(out), ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())

@@ -73,6 +73,8 @@ SIGNATURES = {
     "trex_nk_landscape_loss": (_c_i, [_p, _c_i, _p, _c_i, _c_i, _c_i, _p, _c_i, _p, _p, _c_f,
                                       _c_f, _c_i, _p, _p, _p, _p, _p, _c_i64, _p]),
     "trex_tree_mf_rows": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _p, _p]),
+    "trex_tree_gram_skip_x3": (_c_i, [_p, _c_i, _c_i64, _c_i, _c_f, _p, _p, _c_i64, _p]),
+    "trex_tree_mf_rows_x3": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p, _p]),
     "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),
     "trex_tree_constraint": (_c_i, [_p, _c_i, _c_f, _c_f, _p, _c_i, _p, _p, _p]),
     "trex_tree_compute_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _p, _p, _p]),

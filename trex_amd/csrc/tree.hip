@@ -306,11 +306,40 @@ __device__ __forceinline__ void load_rows8(const float* __restrict__ base, int r
   }
 }
 
+// ---- f16x3 split products (X3 variants) --------------------------------
+// x*s = hi + lo with hi = f16(x*s), lo = f16(x*s - hi): 22 significant bits;
+// x*y ~ hi_x hi_y + hi_x lo_y + lo_x hi_y (lo_x lo_y, ~2^-22 relative, and
+// the split residuals dropped) on v_mfma_f32_32x32x16_f16 with f32
+// accumulation: 3 f16 MFMAs (96 cycles/SIMD) replace 8 f32 ones (512) per
+// 32x32x16 block.  The power-of-two operand scales keep |x*s| <= 2^14 (no
+// f16 overflow) and lo out of the f16 subnormal range; the result is scaled
+// back exactly.  Error per product <~ 1e-6 relative, random in sign: the
+// tests hold these GEMMs to the same rtol 1e-5 vs fp64 as the f32 path.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split_h8(const float (&x)[8], float scale, h8& hi, h8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = x[j] * scale;
+    const _Float16 h = (_Float16)v;
+    hi[j] = h;
+    lo[j] = (_Float16)(v - (float)h);
+  }
+}
+__device__ __forceinline__ f32x16 mfma_x3(const h8& ah, const h8& al, const h8& bh, const h8& bl,
+                                          f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+}
+
+// X3: f16x3 split products; sx, sy operand scales, out scaled by 1/(sx sy)
+template <bool X3>
 __global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ X,
                                                      const float* __restrict__ Y, int N, int K,
                                                      int ntile, int npairs, int symmetric, int t0,
                                                      int ksplit, int kslice,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, float sx = 1.0f,
+                                                     float sy = 1.0f) {
   const int b = blockIdx.x;
   const int xcd = b & 7, m = b >> 3;
   const int split = (m / npairs) * 8 + xcd;
@@ -334,13 +363,27 @@ __global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ 
   };
   auto compute = [&](int kb, float (&xa)[2][8], float (&yb)[2][8]) {
     if (kb >= k_hi) return;
+    if constexpr (X3) {
+      // lane (r, h) holds A[row r][k = 8h + j] and B[k = 8h + j][col r]: the
+      // 32x32x16 f16 fragments are exactly the loaded 8-float runs
+      h8 xh[2], xl[2], yh[2], yl[2];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+      for (int u = 0; u < 2; ++u) split_h8(xa[u], sx, xh[u], xl[u]);
+#pragma unroll
+      for (int v = 0; v < 2; ++v) split_h8(yb[v], sy, yh[v], yl[v]);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
-          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[u][t], yb[v][t], acc[u][v], 0, 0, 0);
+        for (int v = 0; v < 2; ++v) acc[u][v] = mfma_x3(xh[u], xl[u], yh[v], yl[v], acc[u][v]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int v = 0; v < 2; ++v)
+            acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[u][t], yb[v][t], acc[u][v], 0, 0, 0);
+    }
   };
   float xa0[2][8], yb0[2][8], xa1[2][8], yb1[2][8];
   fetch(k_lo, xa0, yb0);
@@ -350,6 +393,7 @@ __global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ 
     fetch(kb + 32, xa0, yb0);
     compute(kb + 16, xa1, yb1);
   }
+  const float unscale = X3 ? 1.0f / (sx * sy) : 1.0f;
   float* out = part + ((size_t)split * npairs + pair) * 64 * 64;
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -358,7 +402,7 @@ __global__ __launch_bounds__(kWave) void gram_kernel2(const float* __restrict__ 
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
-        out[(u * 32 + row) * 64 + v * 32 + r] = acc[u][v][q];
+        out[(u * 32 + row) * 64 + v * 32 + r] = acc[u][v][q] * unscale;
       }
 }
 
@@ -495,10 +539,12 @@ __global__ __launch_bounds__(kWave) void mf_kernel(const float* __restrict__ Mm,
 // step's 32 MFMAs (ping-pong registers, unrolled by two).  Lane (r, h)
 // supplies M[row][nb + 8h + t] and F[nb + 8h + t][col]; rows / n / cols past
 // the edges read a clamped address and contribute 0 (M entry zeroed).
+template <bool X3>
 __global__ __launch_bounds__(kWave) void mf_kernel2(const float* __restrict__ Mm,
                                                    const float* __restrict__ F, int N, int K,
                                                    int row0, int nrows, int nrowt, int ncolb,
-                                                   float* __restrict__ out) {
+                                                   float* __restrict__ out, float sm = 1.0f,
+                                                   float sf = 1.0f) {
   const int b = blockIdx.x;
   const int xcd = b & 7, m = b >> 3;
   const int rt = m % nrowt;
@@ -526,14 +572,23 @@ __global__ __launch_bounds__(kWave) void mf_kernel2(const float* __restrict__ Mm
     fvo[u] = ((8 * h) * K + (col < K ? col : K - 1)) * 4;
   }
   auto fetch = [&](int nb, float (&ma)[2][8], float (&fb)[2][8]) {
+    // M[row][nb + 8h .. +8): two dwordx4 loads per row (rows are only 4-byte
+    // aligned; buffer loads allow that); n past N masked to 0
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int hv = 0; hv < 2; ++hv) {
+        const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rm, mvo[u], (nb + 4 * hv) * 4, 0);
+        const uint32_t e[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int t = 4 * hv + q;
+          ma[u][t] = nb + 8 * h + t < N ? __uint_as_float(e[q]) : 0.0f;
+        }
+      }
+    }
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      const bool nok = nb + 8 * h + t < N;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float mv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rm, mvo[u], (nb + t) * 4, 0));
-        ma[u][t] = nok ? mv : 0.0f;
-      }
 #pragma unroll
       for (int v = 0; v < 2; ++v)
         fb[v][t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rf, fvo[v], (nb + t) * K * 4, 0));
@@ -541,13 +596,25 @@ __global__ __launch_bounds__(kWave) void mf_kernel2(const float* __restrict__ Mm
   };
   auto compute = [&](int nb, float (&ma)[2][8], float (&fb)[2][8]) {
     if (nb >= N) return;
+    if constexpr (X3) {
+      h8 mh[2], ml[2], fh[2], fl[2];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+      for (int u = 0; u < 2; ++u) split_h8(ma[u], sm, mh[u], ml[u]);
+#pragma unroll
+      for (int v = 0; v < 2; ++v) split_h8(fb[v], sf, fh[v], fl[v]);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
-          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(ma[u][t], fb[v][t], acc[u][v], 0, 0, 0);
+        for (int v = 0; v < 2; ++v) acc[u][v] = mfma_x3(mh[u], ml[u], fh[v], fl[v], acc[u][v]);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int v = 0; v < 2; ++v)
+            acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(ma[u][t], fb[v][t], acc[u][v], 0, 0, 0);
+    }
   };
   float ma0[2][8], fb0[2][8], ma1[2][8], fb1[2][8];
   fetch(0, ma0, fb0);
@@ -565,7 +632,7 @@ __global__ __launch_bounds__(kWave) void mf_kernel2(const float* __restrict__ Mm
       for (int q = 0; q < 16; ++q) {
         const int row = rt * 64 + u * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
         const int col = c0 + v * 32 + r;
-        if (row < nrows && col < K) out[(size_t)row * K + col] = acc[u][v][q];
+        if (row < nrows && col < K) out[(size_t)row * K + col] = X3 ? acc[u][v][q] * (1.0f / (sm * sf)) : acc[u][v][q];
       }
 }
 
@@ -859,14 +926,25 @@ extern "C" int64_t trex_tree_workspace_bytes(int N, int64_t K) {
 }
 
 namespace {
+// power of two s with max_abs * s <= 2^14 (f16 split headroom)
+float split_scale(float max_abs) {
+  if (!(max_abs > 0.0f)) return 1.0f;
+  return std::ldexp(1.0f, 14 - (int)std::ceil(std::log2((double)max_abs)));
+}
+
+// x3_max > 0: f16x3 split products with operands bounded by x3_max
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
-         hipStream_t st, int t0 = 0) {
+         hipStream_t st, int t0 = 0, float x3_max = 0.0f) {
   const GramPlan g = gram_plan(N, K, symmetric != 0, t0);
   if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
-  if (K % 16 == 0)
-    hipLaunchKernelGGL(gram_kernel2, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
+  if (K % 16 == 0 && x3_max > 0.0f) {
+    const float sc = split_scale(x3_max);
+    hipLaunchKernelGGL(gram_kernel2<true>, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K,
+                       g.ntile, g.npairs, symmetric, t0, g.ksplit, g.kslice, part, sc, sc);
+  } else if (K % 16 == 0)
+    hipLaunchKernelGGL(gram_kernel2<false>, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
                        g.npairs, symmetric, t0, g.ksplit, g.kslice, part);
   else
     hipLaunchKernelGGL(gram_kernel, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K, g.ntile,
@@ -902,7 +980,7 @@ extern "C" int trex_tree_surrogate(const float* S, const float* A, int N, int64_
     const int nrowt = (N + 63) / 64;
     const int ncolb = (int)((K + 63) / 64);
     const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
-    hipLaunchKernelGGL(mf_kernel2, dim3(blocks), dim3(kWave), 0, st, M, S, N, (int)K, 0, N, nrowt, ncolb,
+    hipLaunchKernelGGL(mf_kernel2<false>, dim3(blocks), dim3(kWave), 0, st, M, S, N, (int)K, 0, N, nrowt, ncolb,
                        dS);
   }
   if (G_out &&
@@ -1015,6 +1093,20 @@ extern "C" int trex_tree_gram_skip(const float* S, int N, int64_t K, int skip_ro
               skip_rows / 64);
 }
 
+extern "C" int trex_tree_gram_skip_x3(const float* S, int N, int64_t K, int skip_rows,
+                                      float max_abs, float* G, void* workspace,
+                                      int64_t workspace_bytes, void* stream) {
+  if (!S || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF || skip_rows < 0 ||
+      skip_rows > N || !(max_abs > 0.0f) || std::isinf(max_abs))
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3: bad arguments");
+  if (K % 16 != 0)
+    return set_error(TREX_E_UNSUPPORTED, "trex_tree_gram_skip_x3: K = L*Q must be a multiple of 16");
+  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3: workspace too small");
+  return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream,
+              skip_rows / 64, max_abs);
+}
+
 extern "C" int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
                               int64_t workspace_bytes, void* stream) {
   return trex_tree_gram_skip(S, N, K, 0, G, workspace, workspace_bytes, stream);
@@ -1042,9 +1134,27 @@ extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t 
   const int nrowt = (nrows + 63) / 64;
   const int ncolb = (int)((K + 63) / 64);
   const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
-  hipLaunchKernelGGL(mf_kernel2, dim3(blocks), dim3(kWave), 0, (hipStream_t)stream, M, S, N,
+  hipLaunchKernelGGL(mf_kernel2<false>, dim3(blocks), dim3(kWave), 0, (hipStream_t)stream, M, S, N,
                      (int)K, row0, nrows, nrowt, ncolb, dS_rows);
   return tree_hip_check("trex_tree_mf_rows");
+}
+
+extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64_t K, int row0,
+                                    int nrows, float max_abs_m, float max_abs_s, float* dS_rows,
+                                    void* stream) {
+  if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
+      row0 + nrows > N || !(max_abs_m > 0.0f) || !(max_abs_s > 0.0f) || std::isinf(max_abs_m) ||
+      std::isinf(max_abs_s))
+    return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3: bad arguments");
+  if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
+    return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows_x3: S exceeds 2 GiB");
+  const int nrowt = (nrows + 63) / 64;
+  const int ncolb = (int)((K + 63) / 64);
+  const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
+  hipLaunchKernelGGL(mf_kernel2<true>, dim3(blocks), dim3(kWave), 0, (hipStream_t)stream, M, S, N,
+                     (int)K, row0, nrows, nrowt, ncolb, dS_rows, split_scale(max_abs_m),
+                     split_scale(max_abs_s));
+  return tree_hip_check("trex_tree_mf_rows_x3");
 }
 
 extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,

@@ -290,10 +290,17 @@ class TreeOptimizer:
     exchange is an all-reduce of the N x N Gram matrix; every rank then
     computes the same loss, dA and tree_params update, and updates its own
     ancestor logits.
+
+    ``gemm``: "x3" (default) runs the two N x N x L*Q GEMMs as f16x3 split
+    products on f16 MFMA (``trex_tree_gram_skip_x3`` / ``trex_tree_mf_rows_x3``;
+    S is a softmax / one-hot, |S| <= 1, and M = diag(r+c) - (A+A^T) with
+    softmax rows, |M| <= N+1, inside their contract), "f32" on f32 MFMA.
+    Both meet the same rtol 1e-5 bar against the fp64 oracle.
     """
 
     def __init__(self, sequences, params: dict, lr: float = 0.01, *,
-                 graph_constraint_scale: float = 10.0, clip_norm=None, group=None):
+                 graph_constraint_scale: float = 10.0, clip_norm=None, group=None,
+                 gemm: str = "x3"):
         torch = _torch()
         self.S = _dev(sequences).clone()  # (N, L, Q): leaf rows fixed, ancestors overwritten
         dev = self.S.device
@@ -323,6 +330,10 @@ class TreeOptimizer:
         self.ws = torch.empty(int(lib().trex_tree_workspace_bytes(self.N, self.K)),
                               dtype=torch.uint8, device=dev)
         self.opt = Adam(self.params, lr, clip_norm=clip_norm)
+        if gemm not in ("x3", "f32"):
+            raise ValueError("gemm must be 'x3' or 'f32'")
+        # the split Gram needs K = L*Q % 16 == 0; otherwise fall back to f32
+        self.gemm = gemm if (gemm == "f32" or self.K % 16 == 0) else "f32"
         # the leaf x leaf block of G = S S^T is constant (leaf rows are data):
         # computed once here, skipped by every step's Gram.  With site
         # sharding the Gram is all-reduced in place, so it is recomputed.
@@ -343,8 +354,12 @@ class TreeOptimizer:
                                       ptr(self.S[self.n_leaf:]), st))
         check(L_.trex_tree_update_tree(ptr(p["tree_params"]), ptr(noise), None, N, self.n_anc,
                                        1.0, ptr(self.A), st))
-        check(L_.trex_tree_gram_skip(ptr(self.S), N, K, self.skip_rows, ptr(self.G),
-                                     ptr(self.ws), self.ws.numel(), st))
+        if self.gemm == "x3":
+            check(L_.trex_tree_gram_skip_x3(ptr(self.S), N, K, self.skip_rows, 1.0, ptr(self.G),
+                                            ptr(self.ws), self.ws.numel(), st))
+        else:
+            check(L_.trex_tree_gram_skip(ptr(self.S), N, K, self.skip_rows, ptr(self.G),
+                                         ptr(self.ws), self.ws.numel(), st))
         if self.reducer is not None:
             self.reducer(self.G)
         check(L_.trex_tree_surrogate_combine(ptr(self.A), ptr(self.G), N, ptr(self.loss),
@@ -352,8 +367,12 @@ class TreeOptimizer:
         check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
                                       ptr(self.dA), ptr(self.ws), st))
         # d loss / dS for the ancestor rows only (leaf rows are fixed data)
-        check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
-                                   ptr(self.dS[self.n_leaf:]), st))
+        if self.gemm == "x3":
+            check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
+                                          float(N + 1), 1.0, ptr(self.dS[self.n_leaf:]), st))
+        else:
+            check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
+                                       ptr(self.dS[self.n_leaf:]), st))
         check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc, 1.0,
                                            ptr(self.grads["tree_params"]), st))
         check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]), ptr(self.dS[self.n_leaf:]),
