@@ -246,6 +246,14 @@ int trex_adam_step(float* params, const float* grads, float* mu, float* nu, int6
                    const double* grad_sq_norm_parts, int n_parts, float clip_norm,
                    void* stream);
 int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts, void* stream);
+/* update_seq's VJP (trex_tree_update_seq_bwd) fused into the Adam update of
+ * the ancestor logits (no clipping): params / mu / nu [n_anc][L][Q] updated
+ * in place from s_anc = softmax(T x) and ds_anc = d loss / d s_anc; the
+ * logits gradient is written to grads_out only when non-NULL.  Bitwise the
+ * same as trex_tree_update_seq_bwd followed by trex_adam_step. */
+int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n_anc, int L, int Q,
+                       float temperature, float* params, float* mu, float* nu, int count,
+                       float lr, float b1, float b2, float eps, float* grads_out, void* stream);
 
 /* ========================================================================
  * Ragged batches: trees of different sizes (n_all_b taxa+ancestors) and

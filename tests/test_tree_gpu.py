@@ -287,3 +287,31 @@ def test_split_gram_and_mf_vs_fp64(device, N, K, skip):
                                      ptr(out), st))
     ref = M.astype(np.float64)[r0:] @ S64
     np.testing.assert_allclose(_n(out), ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("Q,L", [(4, 300), (5, 33)])
+def test_adam_seq_step_fused_is_bitwise_separate(device, Q, L):
+    """trex_adam_seq_step == trex_tree_update_seq_bwd + trex_adam_step, bitwise."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    rng = np.random.default_rng(Q * L)
+    n_anc, T_ = 7, 1.3
+    x = rng.normal(size=(n_anc, L, Q))
+    s_anc = _t(np.exp(x) / np.exp(x).sum(-1, keepdims=True), device)
+    ds = _t(rng.normal(size=(n_anc, L, Q)), device)
+    p0 = _t(rng.normal(size=(n_anc, L, Q)), device)
+    m0 = _t(rng.normal(size=(n_anc, L, Q)) * 0.1, device)
+    v0 = _t(rng.random((n_anc, L, Q)) * 0.1, device)
+    st = stream_handle(torch.device(device))
+    L_ = lib()
+    pa, ma, va = p0.clone(), m0.clone(), v0.clone()
+    g = torch.empty_like(p0)
+    check(L_.trex_tree_update_seq_bwd(ptr(s_anc), ptr(ds), n_anc, L, Q, T_, ptr(g), st))
+    check(L_.trex_adam_step(ptr(pa), ptr(g), ptr(ma), ptr(va), pa.numel(), 3, 0.01, 0.9, 0.999,
+                            1e-8, None, 0, 0.0, st))
+    pb, mb, vb = p0.clone(), m0.clone(), v0.clone()
+    gb = torch.empty_like(p0)
+    check(L_.trex_adam_seq_step(ptr(s_anc), ptr(ds), n_anc, L, Q, T_, ptr(pb), ptr(mb), ptr(vb),
+                                3, 0.01, 0.9, 0.999, 1e-8, ptr(gb), st))
+    assert torch.equal(g, gb) and torch.equal(pa, pb) and torch.equal(ma, mb)
+    assert torch.equal(va, vb)

@@ -789,6 +789,74 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
   }
 }
 
+// update_seq VJP fused into the optax Adam update of the ancestor logits
+// (no clip): g = T s (ds - <s, ds>) per (ancestor, site) row of Q states,
+// then the same Adam arithmetic as adam_kernel; g never touches HBM unless
+// g_out is given.  Q = 4 rows move as float4.
+template <int QT>
+__global__ __launch_bounds__(256) void adam_seq_kernel(const float* __restrict__ s,
+                                                      const float* __restrict__ ds, int64_t rows,
+                                                      int Qr, float T, float* __restrict__ p,
+                                                      float* __restrict__ mu,
+                                                      float* __restrict__ nu, float lr, float b1,
+                                                      float b2, float eps, float bc1, float bc2,
+                                                      float* __restrict__ g_out) {
+  const int Q = QT ? QT : Qr;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
+    float sv[QT ? QT : 32], gv[QT ? QT : 32];
+    if constexpr (QT == 4) {
+      const float4 a = reinterpret_cast<const float4*>(s)[r];
+      const float4 d = reinterpret_cast<const float4*>(ds)[r];
+      sv[0] = a.x; sv[1] = a.y; sv[2] = a.z; sv[3] = a.w;
+      gv[0] = d.x; gv[1] = d.y; gv[2] = d.z; gv[3] = d.w;
+    } else {
+      for (int q = 0; q < Q; ++q) {
+        sv[q] = s[r * Q + q];
+        gv[q] = ds[r * Q + q];
+      }
+    }
+    float dot = sv[0] * gv[0];
+    for (int q = 1; q < Q; ++q) dot = fmaf(sv[q], gv[q], dot);
+    float pv[QT ? QT : 32], mv[QT ? QT : 32], vv[QT ? QT : 32];
+    if constexpr (QT == 4) {
+      const float4 a = reinterpret_cast<const float4*>(p)[r];
+      const float4 m = reinterpret_cast<const float4*>(mu)[r];
+      const float4 v = reinterpret_cast<const float4*>(nu)[r];
+      pv[0] = a.x; pv[1] = a.y; pv[2] = a.z; pv[3] = a.w;
+      mv[0] = m.x; mv[1] = m.y; mv[2] = m.z; mv[3] = m.w;
+      vv[0] = v.x; vv[1] = v.y; vv[2] = v.z; vv[3] = v.w;
+    } else {
+      for (int q = 0; q < Q; ++q) {
+        pv[q] = p[r * Q + q];
+        mv[q] = mu[r * Q + q];
+        vv[q] = nu[r * Q + q];
+      }
+    }
+    for (int q = 0; q < Q; ++q) {
+      const float gt = T * sv[q] * (gv[q] - dot);
+      gv[q] = gt;
+      const float m = (1.0f - b1) * gt + b1 * mv[q];
+      const float v = (1.0f - b2) * (gt * gt) + b2 * vv[q];
+      mv[q] = m;
+      vv[q] = v;
+      pv[q] = pv[q] + (-lr) * ((m / bc1) / (sqrtf(v / bc2) + eps));
+    }
+    if constexpr (QT == 4) {
+      reinterpret_cast<float4*>(p)[r] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+      reinterpret_cast<float4*>(mu)[r] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      reinterpret_cast<float4*>(nu)[r] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      if (g_out) reinterpret_cast<float4*>(g_out)[r] = make_float4(gv[0], gv[1], gv[2], gv[3]);
+    } else {
+      for (int q = 0; q < Q; ++q) {
+        p[r * Q + q] = pv[q];
+        mu[r * Q + q] = mv[q];
+        nu[r * Q + q] = vv[q];
+        if (g_out) g_out[r * Q + q] = gv[q];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void identity_kernel(int N, float* __restrict__ A) {
   const size_t total = (size_t)N * N;
   for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256)
@@ -1060,6 +1128,30 @@ extern "C" int trex_adam_step(float* params, const float* grads, float* mu, floa
                      grads, mu, nu, n, lr, b1, b2, eps, bc1, bc2, grad_sq_norm_parts, n_parts,
                      clip_norm);
   return tree_hip_check("trex_adam_step");
+}
+
+extern "C" int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n_anc, int L,
+                                  int Q, float temperature, float* params, float* mu, float* nu,
+                                  int count, float lr, float b1, float b2, float eps,
+                                  float* grads_out, void* stream) {
+  if (!s_anc || !ds_anc || !params || !mu || !nu || n_anc <= 0 || L <= 0 || Q < 2 || Q > 32 ||
+      count < 1 || !(temperature > 0.0f))
+    return set_error(TREX_E_ARG, "trex_adam_seq_step: bad arguments");
+  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
+  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  const int64_t rows = (int64_t)n_anc * L;
+  const bool al = ((reinterpret_cast<uintptr_t>(s_anc) | reinterpret_cast<uintptr_t>(ds_anc) |
+                    reinterpret_cast<uintptr_t>(params) | reinterpret_cast<uintptr_t>(mu) |
+                    reinterpret_cast<uintptr_t>(nu) | reinterpret_cast<uintptr_t>(grads_out)) &
+                   15) == 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (Q == 4 && al)
+    hipLaunchKernelGGL(adam_seq_kernel<4>, dim3(grid_for(rows)), dim3(256), 0, st, s_anc, ds_anc,
+                       rows, Q, temperature, params, mu, nu, lr, b1, b2, eps, bc1, bc2, grads_out);
+  else
+    hipLaunchKernelGGL(adam_seq_kernel<0>, dim3(grid_for(rows)), dim3(256), 0, st, s_anc, ds_anc,
+                       rows, Q, temperature, params, mu, nu, lr, b1, b2, eps, bc1, bc2, grads_out);
+  return tree_hip_check("trex_adam_seq_step");
 }
 
 extern "C" int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts,

@@ -375,8 +375,24 @@ class TreeOptimizer:
                                        ptr(self.dS[self.n_leaf:]), st))
         check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc, 1.0,
                                            ptr(self.grads["tree_params"]), st))
-        check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]), ptr(self.dS[self.n_leaf:]),
-                                          self.n_anc, self.L, self.Q, T,
-                                          ptr(self.grads["ancestors"]), st))
-        self.opt.step(self.params, self.grads)
+        if self.opt.clip is None:
+            # update_seq VJP fused into the ancestors' Adam update (the logits
+            # gradient never round-trips through HBM); bitwise the same as
+            # update_seq_bwd + Adam.step
+            o = self.opt
+            o.count += 1
+            check(L_.trex_adam_step(ptr(p["tree_params"]), ptr(self.grads["tree_params"]),
+                                    ptr(o.mu["tree_params"]), ptr(o.nu["tree_params"]),
+                                    p["tree_params"].numel(), o.count, float(o.lr), float(o.b1),
+                                    float(o.b2), float(o.eps), None, 0, 0.0, st))
+            check(L_.trex_adam_seq_step(ptr(self.S[self.n_leaf:]), ptr(self.dS[self.n_leaf:]),
+                                        self.n_anc, self.L, self.Q, T, ptr(p["ancestors"]),
+                                        ptr(o.mu["ancestors"]), ptr(o.nu["ancestors"]), o.count,
+                                        float(o.lr), float(o.b1), float(o.b2), float(o.eps),
+                                        None, st))
+        else:
+            check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]),
+                                              ptr(self.dS[self.n_leaf:]), self.n_anc, self.L,
+                                              self.Q, T, ptr(self.grads["ancestors"]), st))
+            self.opt.step(self.params, self.grads)
         return self.loss
