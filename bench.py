@@ -456,15 +456,32 @@ def main():
         with torch.cuda.graph(graph):
             step()
 
+    # N > 1: the step's [dC, loss] all-reduce runs on a side stream and
+    # overlaps the next step's kernel (double-buffered, as DDP overlaps its
+    # gradient buckets with backward); every all-reduce completes inside the
+    # timed region (synchronize at the end waits for both streams)
+    comm = torch.cuda.Stream(device) if world > 1 else None
+    reds = [red, torch.zeros_like(red)]
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    it = [0]
+
     def run_once():
         if graph is not None:
             graph.replay()
         else:
             step()
         if world > 1:
-            red[:Q * Q].copy_(step.out_b["d_cost"].view(-1))
-            red[Q * Q:].copy_(step.out_f["tree_score"].sum().view(1))
-            dist.all_reduce(red)
+            i = it[0] % 2
+            it[0] += 1
+            buf = reds[i]
+            cur = torch.cuda.current_stream(device)
+            cur.wait_event(done[i])  # the all-reduce two steps back has read buf
+            buf[:Q * Q].copy_(step.out_b["d_cost"].view(-1))
+            buf[Q * Q:].copy_(step.out_f["tree_score"].sum().view(1))
+            comm.wait_stream(cur)
+            with torch.cuda.stream(comm):
+                dist.all_reduce(buf)
+                done[i].record(comm)
 
     for _ in range(args.warmup):
         run_once()
@@ -538,7 +555,8 @@ def main():
         "config": {"workload": f"C4 shard per GPU: {B} random {n}-taxa topologies x {L} sites x "
                                f"{Q} states, softmin tau={tau} fwd (DP table written) + grad; "
                                f"global batch {B * world} trees"
-                               + ("; RCCL all-reduce of [dC, loss] per step" if world > 1 else ""),
+                               + ("; RCCL all-reduce of [dC, loss] per step, overlapped with "
+                                  "the next step" if world > 1 else ""),
                    "trees_per_gpu": B, "taxa": n, "sites": L, "states": Q, "tau": tau,
                    "hipgraph": use_graph, "parallelism": f"tree-batch x{world}"},
         "roofline": roofline,
