@@ -302,6 +302,10 @@ def test_c4_scale_properties(device):
     d2, _, _ = eng.backward(lv, c, tau, f2.dp)
     assert torch.equal(f1.tree_score, f2.tree_score) and torch.equal(d1, d2)
     assert torch.equal(f1.dp, f2.dp)
+    # the benchmark's fused kernel at this scale == the separate launches
+    f3, d3f, _, _ = eng.fwd_bwd(lv, c, tau)
+    assert torch.equal(f3.dp, f1.dp) and torch.equal(f3.tree_score, f1.tree_score)
+    assert torch.equal(d3f, d1)
     sample = [0, 17, 63]
     ref = batched_fwd_bwd_ref(ch[sample], leaves[sample], cost, tau)
     np.testing.assert_allclose(f1.tree_score.cpu().numpy()[sample], ref["tree_score"],
@@ -315,10 +319,13 @@ def test_c4_scale_properties(device):
 
 
 @pytest.mark.parametrize("tau", [0.0, 0.5, 0.05])
-def test_fused_fwd_bwd_equals_separate_launches(device, tau):
+@pytest.mark.parametrize("B,L", [(7, 999), (16, 2000)])
+def test_fused_fwd_bwd_equals_separate_launches(device, tau, B, L):
     """trex_sankoff_fwd_bwd == trex_sankoff_fwd + trex_sankoff_bwd, bit for bit
-    (same per-wave arithmetic, same fixed-order reductions)."""
-    B, n, L, Q = 7, 24, 999, 4
+    (same per-wave arithmetic, same fixed-order reductions).  7 x 999 sites
+    is 112 work items (<= one wave per CU: the LDS-resident fused kernel);
+    16 x 2000 is 512 items (the re-reading fused kernel of the benchmark)."""
+    n, Q = 24, 4
     ch = random_topologies(B, n, seed=21)
     leaves = random_leaves(B, n, L, Q, seed=22, missing=0.01)
     cost = int_cost(Q, seed=23, hi=9 if tau == 0.05 else 4)
