@@ -246,6 +246,18 @@ int trex_adam_step(float* params, const float* grads, float* mu, float* nu, int6
                    const double* grad_sq_norm_parts, int n_parts, float clip_norm,
                    void* stream);
 int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts, void* stream);
+/* The optimisers of create_optimizer (src/trex/evals/benchmark.py:41-72),
+ * optax 0.2.6 semantics, one tensor per call, optionally after
+ * clip_by_global_norm (squared-norm partials of ALL gradient tensors):
+ *   kind 0 adam(lr, b1, b2, eps)            state1 = mu, state2 = nu
+ *   kind 1 adamw(lr, b1, b2, eps, wd)       state1 = mu, state2 = nu
+ *   kind 2 sgd(lr, momentum = b1)           state1 = trace
+ *   kind 3 rmsprop(lr, decay = b2, eps)     state2 = nu  (eps inside the sqrt)
+ * count is the 1-based step (bias correction). */
+int trex_optax_step(int kind, float* params, const float* grads, float* state1, float* state2,
+                    int64_t n, int count, float lr, float b1, float b2, float eps,
+                    float weight_decay, const double* grad_sq_norm_parts, int n_parts,
+                    float clip_norm, void* stream);
 /* update_seq's VJP (trex_tree_update_seq_bwd) fused into the Adam update of
  * the ancestor logits (no clipping): params / mu / nu [n_anc][L][Q] updated
  * in place from s_anc = softmax(T x) and ds_anc = d loss / d s_anc; the

@@ -206,3 +206,58 @@ def adam_update(grads, state, lr, b1=0.9, b2=0.999, eps=1e-8, clip_norm=None):
         nh = nu[k] / (1 - b2 ** count)
         upd[k] = -lr * mh / (np.sqrt(nh) + eps)
     return upd, {"count": count, "mu": mu, "nu": nu}
+
+
+# ---------------------------------------------------------------------------
+# create_optimizer (src/trex/evals/benchmark.py:41-72): optax 0.2.6 adam /
+# adamw / sgd(momentum) / rmsprop, optionally chained after
+# clip_by_global_norm(1.0) -- restated from optax's published definitions
+# (third-party, not vendored: "parity unpinned", no reference test checks it)
+# ---------------------------------------------------------------------------
+def optax_init(params):
+    z = {k: np.zeros_like(v, dtype=np.float64) for k, v in params.items()}
+    return {"count": 0, "s1": dict(z), "s2": {k: v.copy() for k, v in z.items()}}
+
+
+def optax_update(name, grads, state, params, lr, clip_norm=1.0, b1=0.9, b2=0.999, eps=1e-8,
+                 weight_decay=0.01, momentum=0.9, decay=0.9):
+    """Returns (updates, state) for name in adam / adamw / sgd / rmsprop."""
+    g = {k: np.asarray(v, dtype=np.float64) for k, v in grads.items()}
+    if clip_norm is not None:
+        norm = np.sqrt(sum(np.sum(v ** 2) for v in g.values()))
+        if not norm < clip_norm:
+            g = {k: v / norm * clip_norm for k, v in g.items()}
+    count = state["count"] + 1
+    s1, s2, upd = {}, {}, {}
+    for k in g:
+        if name in ("adam", "adamw"):
+            m = (1 - b1) * g[k] + b1 * state["s1"][k]
+            v = (1 - b2) * g[k] ** 2 + b2 * state["s2"][k]
+            u = (m / (1 - b1 ** count)) / (np.sqrt(v / (1 - b2 ** count)) + eps)
+            if name == "adamw":
+                u = u + weight_decay * np.asarray(params[k], dtype=np.float64)
+            s1[k], s2[k] = m, v
+        elif name == "sgd":
+            u = g[k] + momentum * state["s1"][k]
+            s1[k], s2[k] = u, state["s2"][k]
+        elif name == "rmsprop":
+            v = decay * state["s2"][k] + (1 - decay) * g[k] ** 2
+            u = g[k] / np.sqrt(v + eps)
+            s1[k], s2[k] = state["s1"][k], v
+        else:
+            raise ValueError(name)
+        upd[k] = -lr * u
+    return upd, {"count": count, "s1": s1, "s2": s2}
+
+
+def fixed_tree_loss_grad(ancestors, masked_sequences, n_leaves, adjacency):
+    """run_trex_optimization_configurable's loss (benchmark.py:158-165):
+    surrogate(update_seq_stacked(ancestors, T=1), A) and d / d ancestors."""
+    anc = np.asarray(ancestors, dtype=np.float64)
+    S = np.array(masked_sequences, dtype=np.float64)
+    P = _softmax(anc)
+    S[n_leaves:] = P
+    A = np.asarray(adjacency, dtype=np.float64)
+    loss, dS, _ = compute_surrogate_cost_grads(S, A)
+    g = dS[n_leaves:]
+    return loss, P * (g - (g * P).sum(-1, keepdims=True))

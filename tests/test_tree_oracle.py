@@ -115,3 +115,15 @@ def test_adam_matches_closed_form_first_steps():
     big = {"x": np.array([30.0, 40.0])}
     u, _ = T.adam_update(big, T.adam_init(p), lr=1.0, clip_norm=1.0)
     np.testing.assert_allclose(u["x"], [-1.0, -1.0], rtol=1e-7)
+
+
+def test_optax_oracle_adam_matches_adam_update():
+    """The generic optax restatement reduces to adam_update for "adam"."""
+    rng = np.random.default_rng(0)
+    p = {"a": rng.normal(size=(3, 4))}
+    st1, st2 = T.adam_init(p), T.optax_init(p)
+    for _ in range(3):
+        g = {"a": rng.normal(size=(3, 4))}
+        u1, st1 = T.adam_update(g, st1, 0.01, clip_norm=1.0)
+        u2, st2 = T.optax_update("adam", g, st2, p, 0.01, clip_norm=1.0)
+        np.testing.assert_allclose(u1["a"], u2["a"], rtol=1e-12)

@@ -789,6 +789,52 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
   }
 }
 
+// optax transformations of src/trex/evals/benchmark.py:41-72
+// (create_optimizer), optionally after clip_by_global_norm:
+//   kind 0 adam(lr, b1, b2, eps)        s1 = mu, s2 = nu (bias-corrected)
+//   kind 1 adamw(lr, ..., wd)           adam + wd * p, then * -lr
+//   kind 2 sgd(lr, momentum = b1)       s1 = trace: t = g + b1 t
+//   kind 3 rmsprop(lr, decay = b2, eps) s2 = nu = b2 nu + (1 - b2) g^2,
+//                                       update g / sqrt(nu + eps)
+// (optax 0.2.6 defaults: eps_root 0, nesterov off, rmsprop eps inside sqrt,
+// initial_scale 0, not centred).
+__global__ __launch_bounds__(256) void optax_kernel(int kind, float* __restrict__ p,
+                                                   const float* __restrict__ g,
+                                                   float* __restrict__ s1,
+                                                   float* __restrict__ s2, int64_t n, float lr,
+                                                   float b1, float b2, float eps, float wd,
+                                                   float bc1, float bc2,
+                                                   const double* __restrict__ sqnorm,
+                                                   int nparts, float clip) {
+  float scale = 1.0f;
+  if (sqnorm) {
+    double sum = 0.0;
+    for (int k = 0; k < nparts; ++k) sum += sqnorm[k];  // same fixed order in every thread
+    const float norm = (float)sqrt(sum);
+    if (!(norm < clip)) scale = clip / norm;
+  }
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const float gt = (scale == 1.0f) ? g[t] : (g[t] / (clip / scale)) * clip;
+    float u;
+    if (kind <= 1) {
+      const float m = (1.0f - b1) * gt + b1 * s1[t];
+      const float v = (1.0f - b2) * (gt * gt) + b2 * s2[t];
+      s1[t] = m;
+      s2[t] = v;
+      u = (m / bc1) / (sqrtf(v / bc2) + eps);
+      if (kind == 1) u = u + wd * p[t];
+    } else if (kind == 2) {
+      u = gt + b1 * s1[t];
+      s1[t] = u;
+    } else {
+      const float v = (1.0f - b2) * (gt * gt) + b2 * s2[t];
+      s2[t] = v;
+      u = gt / sqrtf(v + eps);
+    }
+    p[t] = p[t] + (-lr) * u;
+  }
+}
+
 // update_seq VJP fused into the optax Adam update of the ancestor logits
 // (no clip): g = T s (ds - <s, ds>) per (ancestor, site) row of Q states,
 // then the same Adam arithmetic as adam_kernel; g never touches HBM unless
@@ -1128,6 +1174,21 @@ extern "C" int trex_adam_step(float* params, const float* grads, float* mu, floa
                      grads, mu, nu, n, lr, b1, b2, eps, bc1, bc2, grad_sq_norm_parts, n_parts,
                      clip_norm);
   return tree_hip_check("trex_adam_step");
+}
+
+extern "C" int trex_optax_step(int kind, float* params, const float* grads, float* state1,
+                               float* state2, int64_t n, int count, float lr, float b1, float b2,
+                               float eps, float weight_decay, const double* grad_sq_norm_parts,
+                               int n_parts, float clip_norm, void* stream) {
+  if (kind < 0 || kind > 3 || !params || !grads || n < 0 || count < 1 ||
+      ((kind != 3) && !state1) || ((kind != 2) && !state2))
+    return set_error(TREX_E_ARG, "trex_optax_step: bad arguments");
+  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
+  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  hipLaunchKernelGGL(optax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, kind,
+                     params, grads, state1, state2, n, lr, b1, b2, eps, weight_decay, bc1, bc2,
+                     grad_sq_norm_parts, n_parts, clip_norm);
+  return tree_hip_check("trex_optax_step");
 }
 
 extern "C" int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n_anc, int L,
