@@ -276,14 +276,17 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
 
         group = dist.group.WORLD
     opt = TreeOptimizer(S, params, lr=0.01, group=group)
+    def temp(k):  # the annealing schedule of tests/test_convergence.py:260
+        return max(0.1, 2.0 * (1.0 - k / 5000))
+
     for k in range(warmup):
-        opt.step(max(0.1, 2.0 * (1.0 - k / 5000)), noise[k % 4])
+        opt.step(temp(k), noise[k % 4], next_temperature=temp(k + 1))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(steps):
-        loss = opt.step(max(0.1, 2.0 * (1.0 - (warmup + k) / 5000)), noise[k % 4])
+        loss = opt.step(temp(warmup + k), noise[k % 4], next_temperature=temp(warmup + k + 1))
     torch.cuda.synchronize()
     sec = (time.perf_counter() - t0) / steps
     if world > 1:

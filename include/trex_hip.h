@@ -266,6 +266,16 @@ int trex_optax_step(int kind, float* params, const float* grads, float* state1, 
 int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n_anc, int L, int Q,
                        float temperature, float* params, float* mu, float* nu, int count,
                        float lr, float b1, float b2, float eps, float* grads_out, void* stream);
+/* trex_adam_seq_step with update_seq (src/trex/tree.py:110-130) folded in on
+ * both sides, for a loop whose S rows come from this call: the step's
+ * s_anc = softmax(temperature * params) is recomputed from params (bitwise
+ * what trex_tree_update_seq wrote), and after the Adam update the next
+ * step's rows softmax(next_temperature * params_new) are written to s_next
+ * [n_anc][L][Q] (may be the S buffer the caller's GEMMs read this step). */
+int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, int Q, float temperature,
+                              float next_temperature, float* params, float* mu, float* nu,
+                              int count, float lr, float b1, float b2, float eps, float* s_next,
+                              void* stream);
 
 /* ========================================================================
  * Ragged batches: trees of different sizes (n_all_b taxa+ancestors) and

@@ -211,6 +211,32 @@ def test_tree_optimizer_matches_oracle_loop(device, gemm):
         np.testing.assert_allclose(_n(opt.params[k]), p_ref[k], rtol=5e-5, atol=5e-6)
 
 
+@pytest.mark.parametrize("Q", [4, 5])
+def test_tree_optimizer_next_temperature_hint_is_bitwise_neutral(device, Q):
+    """update_seq folded into the Adam kernel (trex_adam_seq_update_step,
+    used when step() knows the next temperature) gives bitwise the same
+    losses and parameters as recomputing S at the start of every step --
+    including a wrong hint, which must only cost a recompute."""
+    L = 48 if Q == 4 else 32  # K = 192 / 160
+    params, noise, seqs = _tree_case(16, L, Q, 5)
+    nz = _t(noise, device)
+    temps = [2.0, 1.5, 1.5, 1.2, 0.9, 0.9]
+    runs = []
+    for mode in ("hint", "none", "wrong"):
+        opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                              lr=0.01)
+        losses = []
+        for i, Tt in enumerate(temps):
+            nxt = temps[i + 1] if i + 1 < len(temps) else Tt
+            hint = {"hint": nxt, "none": None, "wrong": nxt + 0.25}[mode]
+            losses.append(float(opt.step(Tt, nz, next_temperature=hint)))
+        runs.append((losses, {k: v.clone() for k, v in opt.params.items()}))
+    for losses, prm in runs[1:]:
+        assert losses == runs[0][0]
+        for k in prm:
+            assert torch.equal(prm[k], runs[0][1][k])
+
+
 @pytest.mark.parametrize("N,K,row0", [(511, 4096, 256), (100, 132, 37), (64, 64, 0)])
 def test_mf_rows_equals_full_dS_slice(device, N, K, row0):
     """trex_tree_mf_rows (the optimiser's ancestor-rows-only dS = M S) is
@@ -252,7 +278,8 @@ def test_gram_skip_keeps_cached_block(device):
     assert torch.equal(G[mask], full[mask])
 
 
-@pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (100, 1024, 0), (64, 16, 0)])
+@pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 160, 130),
+                                      (100, 1024, 0), (64, 16, 0)])
 def test_split_gram_and_mf_vs_fp64(device, N, K, skip):
     """f16x3 split-product Gram / MF (trex_tree_gram_skip_x3 /
     trex_tree_mf_rows_x3) vs fp64 at the f32 path's bar: softmax-like S
@@ -281,12 +308,12 @@ def test_split_gram_and_mf_vs_fp64(device, N, K, skip):
     mask = np.ones((N, N), bool)
     mask[:t0, :t0] = False
     np.testing.assert_allclose(_n(Gx)[mask], Gref[mask], rtol=1e-5, atol=1e-5 * Gref.max())
-    r0 = N // 2
-    out = torch.empty((N - r0, K), device=device)
-    check(lib().trex_tree_mf_rows_x3(ptr(Mt), ptr(St), N, K, r0, N - r0, float(N + 1), 1.0,
-                                     ptr(out), st))
-    ref = M.astype(np.float64)[r0:] @ S64
-    np.testing.assert_allclose(_n(out), ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+    for r0 in (N // 2, 0):  # 0: more than 256 output rows for N = 511 / 300
+        out = torch.empty((N - r0, K), device=device)
+        check(lib().trex_tree_mf_rows_x3(ptr(Mt), ptr(St), N, K, r0, N - r0, float(N + 1), 1.0,
+                                         ptr(out), st))
+        ref = M.astype(np.float64)[r0:] @ S64
+        np.testing.assert_allclose(_n(out), ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
 
 
 @pytest.mark.parametrize("Q,L", [(4, 300), (5, 33)])

@@ -83,6 +83,8 @@ SIGNATURES = {
     "trex_sq_norm_parts": (_c_i, [_p, _c_i64, _p, _c_i, _p]),
     "trex_optax_step": (_c_i, [_c_i, _p, _p, _p, _p, _c_i64, _c_i, _c_f, _c_f, _c_f, _c_f, _c_f,
                                _p, _c_i, _c_f, _p]),
+    "trex_adam_seq_update_step": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _c_f, _p, _p, _p, _c_i, _c_f,
+                                         _c_f, _c_f, _c_f, _p, _p]),
     "trex_adam_seq_step": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_f, _p, _p, _p, _c_i, _c_f, _c_f,
                                   _c_f, _c_f, _p, _p]),
 }

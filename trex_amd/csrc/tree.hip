@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "sankoff_dev.h"
 #include "trex_common.h"
@@ -427,6 +428,181 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
   }
 }
 
+// ---- v3 Gram: LDS-staged K chunks, one workgroup per CU -------------------
+// Symmetric G = S S^T (f16x3 split products) over the needed 32x32 tiles:
+// the upper triangle minus the cached leaf x leaf block (tiles with both
+// strips < t0s), enumerated row-major like pair_tiles.  A workgroup is 8
+// waves, two per SIMD (256 registers each, no spills): a wave owns up to 13
+// tiles (208 accumulator registers); a workgroup owns up to 104 tiles (a
+// "group"; more tiles -> more groups; C5's 100 tiles are one) and a
+// contiguous range of 16-wide K chunks (its split), one workgroup per CU.
+// Per chunk all N <= 512 rows are loaded ONCE from HBM (one dwordx4 per
+// thread per 128 rows, issued a chunk ahead into
+// registers), split into f16 hi / lo planes in LDS (double-buffered, row
+// stride 80 B: hi k0..15 | lo k0..15 | pad), and every wave feeds its
+// tiles' 32x32x16 MFMAs from LDS fragments (the A fragment re-read only when
+// the tile row strip changes).  The v2 kernel instead re-read each row once
+// per 64x64 tile pair from L2 with one wave per pair: load-bound.
+// Partials [split][tile][32][32] (scaled back) reduce in a fixed order.
+constexpr int kG3Rows = 512;
+constexpr int kG3Stride = 80;
+constexpr int kG3Tiles = 13;
+constexpr int kG3Waves = 8;
+constexpr int kG3Buf = kG3Rows * kG3Stride;
+constexpr int kG3Lds = 2 * kG3Buf;
+
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+// workgroup barrier for LDS hand-over only: waits for this wave's LDS ops
+// (lgkmcnt) but NOT for its outstanding global loads -- __syncthreads()'s
+// fence would drain vmcnt and so the register prefetch of the next chunk
+// at every barrier
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ void g3_stage(unsigned char* buf, int row, int sub, const u32x4& w,
+                                         float sc) {
+  const float v[4] = {__uint_as_float(w.x) * sc, __uint_as_float(w.y) * sc,
+                      __uint_as_float(w.z) * sc, __uint_as_float(w.w) * sc};
+  h4 hi, lo;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hi[j] = (_Float16)v[j];
+    lo[j] = (_Float16)(v[j] - (float)hi[j]);
+  }
+  *reinterpret_cast<h4*>(buf + row * kG3Stride + sub * 8) = hi;
+  *reinterpret_cast<h4*>(buf + row * kG3Stride + 32 + sub * 8) = lo;
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gram_kernel3(
+    const float* __restrict__ S, int N, int K, int ns, int t0s, int ntiles, int ngroups,
+    int ksplit, int nchunks, float sc, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds3[];
+  const int g = blockIdx.x % ngroups;
+  const int split = blockIdx.x / ngroups;
+  const int c_lo = (int)((int64_t)split * nchunks / ksplit);
+  const int c_hi = (int)((int64_t)(split + 1) * nchunks / ksplit);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int tb = (g * kG3Waves + wave) * kG3Tiles;
+  const int nt = max(0, min(kG3Tiles, ntiles - tb));
+  // first tile's strips; tiles past the wave's range (t >= nt) run on
+  // whatever strips follow (clamped to ns - 1) and are not written: every
+  // wave issues the same unconditional MFMA stream
+  int a0, b0;
+  pair_tiles(min(tb, ntiles - 1), ns, 1, t0s, &a0, &b0);
+
+  f32x16 acc[kG3Tiles];
+#pragma unroll
+  for (int t = 0; t < kG3Tiles; ++t) acc[t] = (f32x16){};
+
+  // loads: thread (rb = tid / 4, sub = tid % 4) fetches S[rb + 128 i][k0 + 4 sub .. + 4);
+  // rows past N read out of bounds (0)
+  const rsrc_t rs = make_rsrc(S, (uint32_t)((size_t)N * K * 4));
+  const int sub = tid & 3, rb = tid >> 2;
+  constexpr int kRowsPerPass = kG3Waves * kWave / 4;
+  u32x4 pf[kG3Rows / kRowsPerPass];
+  auto gload = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < kG3Rows / kRowsPerPass; ++i)
+      pf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((rb + kRowsPerPass * i) * K + 4 * sub) * 4,
+                                                    c * 64, 0);
+  };
+  auto stage = [&](unsigned char* buf) {
+#pragma unroll
+    for (int i = 0; i < kG3Rows / kRowsPerPass; ++i)
+      g3_stage(buf, rb + kRowsPerPass * i, sub, pf[i], sc);
+  };
+  const int lofs = r * kG3Stride + 16 * h;
+  auto compute = [&](const unsigned char* buf) {
+    int a = a0, b = b0;
+#pragma unroll
+    for (int t = 0; t < kG3Tiles; ++t) {
+      const unsigned char* pa = buf + a * (32 * kG3Stride) + lofs;
+      const unsigned char* pb = buf + b * (32 * kG3Stride) + lofs;
+      const h8 ah = *reinterpret_cast<const h8*>(pa);
+      const h8 al = *reinterpret_cast<const h8*>(pa + 32);
+      const h8 bh = *reinterpret_cast<const h8*>(pb);
+      const h8 bl = *reinterpret_cast<const h8*>(pb + 32);
+      acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
+      if (++b >= ns) {
+        a = min(a + 1, ns - 1);
+        b = a > t0s ? a : t0s;
+      }
+    }
+  };
+
+  if (c_lo < c_hi) {
+    gload(c_lo);
+    stage(lds3);
+    if (c_lo + 1 < c_hi) gload(c_lo + 1);
+  }
+  lds_barrier();
+  for (int c = c_lo; c < c_hi; ++c) {
+    unsigned char* cb = lds3 + ((c - c_lo) & 1) * kG3Buf;
+    unsigned char* nb = lds3 + (((c - c_lo) & 1) ^ 1) * kG3Buf;
+    compute(cb);
+    if (c + 1 < c_hi) {
+      stage(nb);
+      if (c + 2 < c_hi) gload(c + 2);
+    }
+    lds_barrier();
+  }
+
+  const float unscale = 1.0f / (sc * sc);
+#pragma unroll
+  for (int t = 0; t < kG3Tiles; ++t) {
+    if (t < nt) {
+      float* out = part + ((size_t)split * ntiles + tb + t) * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+        out[row * 32 + r] = acc[t][q] * unscale;
+      }
+    }
+  }
+}
+
+// G[i][j] = G[j][i] = sum over splits of the v3 partials, fp64 in a fixed
+// association: thread (e, q) of a block (64 elements x 4 quarters) sums the
+// splits sp = q, q + 4, ... in order (4 independent loads in flight), then
+// the four quarter sums add in q order.  One wave reads 256 contiguous bytes
+// per split; the grid has ntiles * 16 waves (the serial one-thread-per-
+// element loop kept too few loads in flight: 1.4 TB/s).
+__global__ __launch_bounds__(256) void gram3_reduce_kernel(const float* __restrict__ part, int N,
+                                                          int ns, int t0s, int ntiles,
+                                                          int ksplit, float* __restrict__ G) {
+  __shared__ double qs[4][64];
+  const int el = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const size_t t = (size_t)blockIdx.x * 64 + el;  // element index, < ntiles * 1024
+  const size_t stride = (size_t)ntiles * 1024;
+  const float* src = part + t;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int sp = q;
+  for (; sp + 12 < ksplit; sp += 16) {
+    s0 += (double)src[(size_t)sp * stride];
+    s1 += (double)src[(size_t)(sp + 4) * stride];
+    s2 += (double)src[(size_t)(sp + 8) * stride];
+    s3 += (double)src[(size_t)(sp + 12) * stride];
+  }
+  for (; sp < ksplit; sp += 4) s0 += (double)src[(size_t)sp * stride];
+  qs[q][el] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (q != 0) return;
+  const double s = ((qs[0][el] + qs[1][el]) + qs[2][el]) + qs[3][el];
+  const int tile = (int)(t >> 10);
+  const int e = (int)(t & 1023);
+  int si, sj;
+  pair_tiles(tile, ns, 1, t0s, &si, &sj);
+  const int i = si * 32 + (e >> 5), j = sj * 32 + (e & 31);
+  if (i < N && j < N) {
+    G[(size_t)i * N + j] = (float)s;
+    G[(size_t)j * N + i] = (float)s;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // a9 combine: per row i (one block): rowloss_i, dA row, M row.
 //   loss = sum_ij A_ij (G_ii + G_jj - 2 G_ij) / 2 ; dA_ij = (G_ii+G_jj)/2 - G_ij
@@ -634,6 +810,168 @@ __global__ __launch_bounds__(kWave) void mf_kernel2(const float* __restrict__ Mm
         const int col = c0 + v * 32 + r;
         if (row < nrows && col < K) out[(size_t)row * K + col] = X3 ? acc[u][v][q] * (1.0f / (sm * sf)) : acc[u][v][q];
       }
+}
+
+// ---- v3 MF: out = M[row0 : row0 + nrows] F, LDS-staged F slices ----------
+// A workgroup (8 waves, two per SIMD) owns TPC x 32 output columns and up to
+// 256 output rows (wave w: rows 32w .. 32w + 31 x all TPC column tiles).
+// It walks n in stages of 32 (two 32x32x16 k-steps): the F slice
+// F[n .. n+32)[columns] is loaded ONCE per workgroup from HBM (item (p, cg):
+// rows 2p, 2p + 1, columns 4cg .. 4cg + 3; 64 B runs per row), split into f16 hi /
+// lo and stored column-major in LDS (column stride 144 B: hi n0..31 | lo
+// n0..31 | pad; two n per 32-bit write), so every B fragment is one
+// ds_read_b128; each wave's M fragment (its 32 rows, L2 resident) is loaded
+// directly and split in registers.  Pipeline: F of stages s+1 and s+2 and M
+// of s+1 are in flight while stage s computes (two register sets, loop
+// unrolled by two, loads issued M(x) then F(x+1) so the in-order vmcnt wait
+// for one never waits for the other); LDS double-buffered, one barrier per
+// stage.  All offsets are in voffset, so rows / n past N read out of bounds
+// (0).  TPC is picked per launch so the column tiles divide evenly over the
+// CUs (C5: 6 250 tiles -> 1 250 workgroups of 5 = 5 rounds of 256).  The v2
+// kernel issued one 4-byte load per F element per wave: load-bound.
+constexpr int kMfStride = 144;
+
+template <int TPC>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void mf_kernel3(
+    const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
+    float* __restrict__ out, float sm, float sf) {
+  constexpr int CW = TPC * 32;
+  constexpr int NIT = 16 * (CW / 4);  // (row pair, column group) items per stage
+  constexpr int IPT = (NIT + 511) / 512;
+  constexpr int BUF = CW * kMfStride;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ldsm[];
+  const int c0 = blockIdx.x * CW;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int orow = blockIdx.y * 256 + wave * 32 + r;  // this lane's output row (A fragment row)
+  const rsrc_t rm = make_rsrc(Mm, (uint32_t)((size_t)N * N * 4));
+  const rsrc_t rf = make_rsrc(F, (uint32_t)((size_t)N * K * 4));
+  // sentinel leaves room for the small per-load additions below (no int wrap)
+  const int mvo = orow < nrows ? ((row0 + orow) * N + 8 * h) * 4 : 0x7FFF0000;
+  int fvo[IPT], lofs[IPT];
+  bool fok[IPT];
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int item = tid + 512 * j;
+    fok[j] = item < NIT;
+    // p fastest: the 16 lanes of one column group write 16 consecutive LDS
+    // dwords (conflict-free; cg fastest was a 16-way bank conflict), and
+    // read 64 contiguous bytes per F row
+    const int p = fok[j] ? item % 16 : 0, cg = fok[j] ? item / 16 : 0;
+    fvo[j] = ((2 * p) * K + c0 + 4 * cg) * 4;
+    lofs[j] = 4 * cg * kMfStride + 4 * p;
+  }
+  const int nst = (N + 31) / 32;
+
+  f32x16 acc[TPC];
+#pragma unroll
+  for (int t = 0; t < TPC; ++t) acc[t] = (f32x16){};
+
+  struct FSet { u32x4 a[IPT], b[IPT]; };
+  struct MSet { u32x4 m[4]; };
+  FSet f0, f1;
+  MSet m0, m1;
+  auto fload = [&](int s, FSet& f) {
+    const int so = s * 32 * K * 4;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      const int vo = fok[j] ? fvo[j] + so : 0x7FFF0000;
+      f.a[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, vo, 0, 0);
+      f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, fok[j] ? vo + K * 4 : vo, 0, 0);
+    }
+  };
+  auto mload = [&](int s, MSet& m) {
+    const int vo = mvo == 0x7FFF0000 ? mvo : mvo + s * 128;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      m.m[kk] = __builtin_amdgcn_raw_buffer_load_b128(rm, vo + (kk >> 1) * 64 + (kk & 1) * 16, 0, 0);
+  };
+  auto stage = [&](unsigned char* buf, const FSet& f) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      if (!fok[j]) continue;
+      const uint32_t a[4] = {f.a[j].x, f.a[j].y, f.a[j].z, f.a[j].w};
+      const uint32_t b[4] = {f.b[j].x, f.b[j].y, f.b[j].z, f.b[j].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float va = __uint_as_float(a[c]) * sf, vb = __uint_as_float(b[c]) * sf;
+        const _Float16 ha = (_Float16)va, hb = (_Float16)vb;
+        const _Float16 la = (_Float16)(va - (float)ha), lb = (_Float16)(vb - (float)hb);
+        unsigned char* col = buf + lofs[j] + c * kMfStride;
+        *reinterpret_cast<h2*>(col) = (h2){ha, hb};
+        *reinterpret_cast<h2*>(col + 64) = (h2){la, lb};
+      }
+    }
+  };
+  auto compute = [&](const unsigned char* buf, int s, const MSet& m) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const u32x4 w0 = m.m[2 * kk], w1 = m.m[2 * kk + 1];
+      const uint32_t e[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      float mv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        mv[j] = (s * 32 + kk * 16 + 8 * h + j < N) ? __uint_as_float(e[j]) : 0.0f;
+      h8 ah, al;
+      split_h8(mv, sm, ah, al);
+      const unsigned char* pb = buf + r * kMfStride + kk * 32 + 16 * h;
+#pragma unroll
+      for (int t = 0; t < TPC; ++t) {
+        const h8 bh = *reinterpret_cast<const h8*>(pb + t * 32 * kMfStride);
+        const h8 bl = *reinterpret_cast<const h8*>(pb + t * 32 * kMfStride + 64);
+        acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
+      }
+    }
+  };
+
+  unsigned char* buf0 = ldsm;
+  unsigned char* buf1 = ldsm + BUF;
+  // issue order F(0) M(0) F(1) M(1) F(2) ..., i.e. M(x) before F(x + 1)
+  fload(0, f0);
+  mload(0, m0);
+  fload(1, f1);
+  stage(buf0, f0);
+  mload(1, m1);
+  fload(2, f0);
+  lds_barrier();
+  for (int s = 0; s < nst; s += 2) {
+    compute(buf0, s, m0);
+    if (s + 1 < nst) stage(buf1, f1);
+    mload(s + 2, m0);
+    fload(s + 3, f1);
+    lds_barrier();
+    if (s + 1 >= nst) break;
+    compute(buf1, s + 1, m1);
+    if (s + 2 < nst) stage(buf0, f0);
+    mload(s + 3, m1);
+    fload(s + 4, f0);
+    lds_barrier();
+  }
+
+  const float unscale = 1.0f / (sm * sf);
+  if (blockIdx.y * 256 + wave * 32 >= nrows) return;
+#pragma unroll
+  for (int t = 0; t < TPC; ++t) {
+    const int col = c0 + t * 32 + r;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = blockIdx.y * 256 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (row < nrows && col < K) out[(size_t)row * K + col] = acc[t][q] * unscale;
+    }
+  }
+}
+
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
 }
 
 // ---------------------------------------------------------------------------
@@ -903,6 +1241,85 @@ __global__ __launch_bounds__(256) void adam_seq_kernel(const float* __restrict__
   }
 }
 
+// One ancestor-logits step with update_seq folded in on both sides: s =
+// softmax(T p) recomputed from the logits it reads anyway (the same
+// arithmetic as update_seq_kernel, so bitwise the S the step's GEMMs used),
+// the VJP g = T s (ds - <s, ds>), the Adam update of p / mu / nu, and the
+// NEXT step's S rows softmax(Tn p_new) written to s_out: per row of Q
+// logits 16 B of ds + 12 B of Adam state in, 16 B + 12 B out, no separate
+// update_seq pass (which re-read p) and no read of the old S.
+__device__ __forceinline__ void softmax4(const float (&x)[4], float T, float (&o)[4]) {
+  const float a = x[0] * T, b = x[1] * T, c = x[2] * T, d = x[3] * T;
+  const float m = fmaxf(fmaxf(a, b), fmaxf(c, d));
+  const float ea = expf(a - m), eb = expf(b - m), ec = expf(c - m), ed = expf(d - m);
+  const float inv = 1.0f / (((ea + eb) + ec) + ed);
+  o[0] = ea * inv; o[1] = eb * inv; o[2] = ec * inv; o[3] = ed * inv;
+}
+__device__ __forceinline__ void softmaxq(const float* x, int Q, float T, float* o) {
+  float m = -INFINITY;
+  for (int q = 0; q < Q; ++q) m = fmaxf(m, x[q] * T);
+  float sum = 0.0f;
+  for (int q = 0; q < Q; ++q) sum += expf(x[q] * T - m);
+  const float inv = 1.0f / sum;
+  for (int q = 0; q < Q; ++q) o[q] = expf(x[q] * T - m) * inv;
+}
+
+template <int QT>
+__global__ __launch_bounds__(256) void adam_seq_update_kernel(
+    const float* __restrict__ ds, int64_t rows, int Qr, float T, float Tn, float* __restrict__ p,
+    float* __restrict__ mu, float* __restrict__ nu, float lr, float b1, float b2, float eps,
+    float bc1, float bc2, float* __restrict__ s_out) {
+  const int Q = QT ? QT : Qr;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
+    float pv[QT ? QT : 32], mv[QT ? QT : 32], vv[QT ? QT : 32], gv[QT ? QT : 32],
+        sv[QT ? QT : 32];
+    if constexpr (QT == 4) {
+      const float4 a = reinterpret_cast<const float4*>(p)[r];
+      const float4 d = reinterpret_cast<const float4*>(ds)[r];
+      const float4 m = reinterpret_cast<const float4*>(mu)[r];
+      const float4 v = reinterpret_cast<const float4*>(nu)[r];
+      pv[0] = a.x; pv[1] = a.y; pv[2] = a.z; pv[3] = a.w;
+      gv[0] = d.x; gv[1] = d.y; gv[2] = d.z; gv[3] = d.w;
+      mv[0] = m.x; mv[1] = m.y; mv[2] = m.z; mv[3] = m.w;
+      vv[0] = v.x; vv[1] = v.y; vv[2] = v.z; vv[3] = v.w;
+      softmax4(pv, T, sv);
+    } else {
+      for (int q = 0; q < Q; ++q) {
+        pv[q] = p[r * Q + q];
+        gv[q] = ds[r * Q + q];
+        mv[q] = mu[r * Q + q];
+        vv[q] = nu[r * Q + q];
+      }
+      softmaxq(pv, Q, T, sv);
+    }
+    float dot = sv[0] * gv[0];
+    for (int q = 1; q < Q; ++q) dot = fmaf(sv[q], gv[q], dot);
+    for (int q = 0; q < Q; ++q) {
+      const float gt = T * sv[q] * (gv[q] - dot);
+      const float m = (1.0f - b1) * gt + b1 * mv[q];
+      const float v = (1.0f - b2) * (gt * gt) + b2 * vv[q];
+      mv[q] = m;
+      vv[q] = v;
+      pv[q] = pv[q] + (-lr) * ((m / bc1) / (sqrtf(v / bc2) + eps));
+    }
+    if constexpr (QT == 4) {
+      softmax4(pv, Tn, sv);
+      reinterpret_cast<float4*>(p)[r] = make_float4(pv[0], pv[1], pv[2], pv[3]);
+      reinterpret_cast<float4*>(mu)[r] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      reinterpret_cast<float4*>(nu)[r] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      reinterpret_cast<float4*>(s_out)[r] = make_float4(sv[0], sv[1], sv[2], sv[3]);
+    } else {
+      softmaxq(pv, Q, Tn, sv);
+      for (int q = 0; q < Q; ++q) {
+        p[r * Q + q] = pv[q];
+        mu[r * Q + q] = mv[q];
+        nu[r * Q + q] = vv[q];
+        s_out[r * Q + q] = sv[q];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void identity_kernel(int N, float* __restrict__ A) {
   const size_t total = (size_t)N * N;
   for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256)
@@ -1017,6 +1434,24 @@ GramPlan gram_plan(int N, int64_t K, bool symmetric = false, int t0 = 0) {
   g.ksplit = (int)((K + g.kslice - 1) / g.kslice);
   return g;
 }
+
+// v3 plan (symmetric, N <= 512, K % 16 == 0): 32-row strips, tiles per
+// group of 8 waves x 13, about one workgroup per CU
+struct Gram3Plan {
+  int ns, t0s, ntiles, ngroups, ksplit, nchunks;
+};
+Gram3Plan gram3_plan(int N, int64_t K, int t0s) {
+  Gram3Plan g;
+  g.ns = (N + 31) / 32;
+  g.t0s = t0s;
+  g.ntiles = 0;
+  for (int a = 0; a < g.ns; ++a) g.ntiles += sym_row_len(a, g.ns, t0s);
+  g.ngroups = std::max(1, (g.ntiles + kG3Waves * kG3Tiles - 1) / (kG3Waves * kG3Tiles));
+  g.nchunks = (int)(K / 16);
+  g.ksplit = std::max(1, std::min(g.nchunks, std::max(1, 256 / g.ngroups)));
+  return g;
+}
+bool gram3_ok(int N, int64_t K) { return N <= kG3Rows && K % 16 == 0 && (int64_t)N * K * 4 < 0x7FFFFFF0LL; }
 }  // namespace
 
 namespace {
@@ -1026,6 +1461,15 @@ int64_t part_bytes(int N, int64_t K) {
   for (bool sym : {true, false}) {
     const GramPlan g = gram_plan(N, K, sym);
     b = std::max<int64_t>(b, (int64_t)((g.ksplit + 7) / 8 * 8) * g.npairs * 4096 * 4);
+  }
+  if (gram3_ok(N, K)) {
+    // every skip (t0s) the v3 path can be given: more skipped tiles can
+    // mean fewer groups and so more splits
+    const int ns = (N + 31) / 32;
+    for (int t0s = 0; t0s <= ns; ++t0s) {
+      const Gram3Plan g = gram3_plan(N, K, t0s);
+      b = std::max<int64_t>(b, (int64_t)g.ksplit * g.ntiles * 4096);
+    }
   }
   return b;
 }
@@ -1046,6 +1490,16 @@ float split_scale(float max_abs) {
   return std::ldexp(1.0f, 14 - (int)std::ceil(std::log2((double)max_abs)));
 }
 
+// TREX_GRAM_V2=1 keeps the v2 x3 Gram and MF kernels (one wave per 64x64
+// tile, operands straight from L2), for A/B
+bool gram_v2_forced() {
+  static const bool f = [] {
+    const char* e = std::getenv("TREX_GRAM_V2");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
+
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
          hipStream_t st, int t0 = 0, float x3_max = 0.0f) {
@@ -1053,6 +1507,22 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
   if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
+  if (symmetric && X == Y && x3_max > 0.0f && gram3_ok(N, K) && !gram_v2_forced()) {
+    const Gram3Plan p = gram3_plan(N, K, 2 * t0);
+    if (p.ntiles == 0) return TREX_OK;
+    static bool lds_set = false;
+    if (!lds_set) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
+      lds_set = true;
+    }
+    hipLaunchKernelGGL(gram_kernel3, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds, st, X, N,
+                       (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks,
+                       split_scale(x3_max), part);
+    hipLaunchKernelGGL(gram3_reduce_kernel, dim3(p.ntiles * 16), dim3(256), 0, st, part, N, p.ns,
+                       p.t0s, p.ntiles, p.ksplit, G);
+    return tree_hip_check("gram");
+  }
   if (K % 16 == 0 && x3_max > 0.0f) {
     const float sc = split_scale(x3_max);
     hipLaunchKernelGGL(gram_kernel2<true>, dim3(blocks), dim3(kWave), 0, st, X, Y, N, (int)K,
@@ -1215,6 +1685,32 @@ extern "C" int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n
   return tree_hip_check("trex_adam_seq_step");
 }
 
+extern "C" int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, int Q,
+                                         float temperature, float next_temperature,
+                                         float* params, float* mu, float* nu, int count, float lr,
+                                         float b1, float b2, float eps, float* s_next,
+                                         void* stream) {
+  if (!ds_anc || !params || !mu || !nu || !s_next || n_anc <= 0 || L <= 0 || Q < 2 || Q > 32 ||
+      count < 1 || !(temperature > 0.0f) || !(next_temperature > 0.0f))
+    return set_error(TREX_E_ARG, "trex_adam_seq_update_step: bad arguments");
+  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
+  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  const int64_t rows = (int64_t)n_anc * L;
+  const bool al = ((reinterpret_cast<uintptr_t>(ds_anc) | reinterpret_cast<uintptr_t>(params) |
+                    reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
+                    reinterpret_cast<uintptr_t>(s_next)) & 15) == 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (Q == 4 && al)
+    hipLaunchKernelGGL(adam_seq_update_kernel<4>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
+                       rows, Q, temperature, next_temperature, params, mu, nu, lr, b1, b2, eps,
+                       bc1, bc2, s_next);
+  else
+    hipLaunchKernelGGL(adam_seq_update_kernel<0>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
+                       rows, Q, temperature, next_temperature, params, mu, nu, lr, b1, b2, eps,
+                       bc1, bc2, s_next);
+  return tree_hip_check("trex_adam_seq_update_step");
+}
+
 extern "C" int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts,
                                   void* stream) {
   if (!x || !parts || n_parts <= 0 || n_parts > 8192)
@@ -1301,6 +1797,30 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
     return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3: bad arguments");
   if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
     return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows_x3: S exceeds 2 GiB");
+  if (!gram_v2_forced()) {
+    // column tiles per workgroup: fewest rounds x tiles over one workgroup per CU
+    const int64_t ct = (K + 31) / 32;
+    const int rg = (nrows + 255) / 256;
+    int best = 5;
+    int64_t best_cost = INT64_MAX;
+    for (int tpc : {5, 4}) {
+      const int64_t wgs = (ct + tpc - 1) / tpc * rg;
+      const int64_t cost = (wgs + cu_count() - 1) / cu_count() * tpc;
+      if (cost < best_cost) { best_cost = cost; best = tpc; }
+    }
+    auto go = [&](auto kernel, int tpc) {
+      const int lds = 2 * tpc * 32 * kMfStride;
+      if (lds > 65536)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(kernel, dim3((unsigned)((ct + tpc - 1) / tpc), rg), dim3(512), lds,
+                         (hipStream_t)stream, M, S, N, (int)K, row0, nrows, dS_rows,
+                         split_scale(max_abs_m), split_scale(max_abs_s));
+    };
+    if (best == 5) go(mf_kernel3<5>, 5);
+    else go(mf_kernel3<4>, 4);
+    return tree_hip_check("trex_tree_mf_rows_x3");
+  }
   const int nrowt = (nrows + 63) / 64;
   const int ncolb = (int)((K + 63) / 64);
   const int blocks = nrowt * ((ncolb + 7) / 8 * 8);

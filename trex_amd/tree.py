@@ -330,6 +330,7 @@ class TreeOptimizer:
         self.ws = torch.empty(int(lib().trex_tree_workspace_bytes(self.N, self.K)),
                               dtype=torch.uint8, device=dev)
         self.opt = Adam(self.params, lr, clip_norm=clip_norm)
+        self._s_temperature = None  # temperature the S ancestor rows were computed with
         if gemm not in ("x3", "f32"):
             raise ValueError("gemm must be 'x3' or 'f32'")
         # the split Gram needs K = L*Q % 16 == 0; otherwise fall back to f32
@@ -343,15 +344,24 @@ class TreeOptimizer:
                                        self.ws.numel(), stream_handle(dev)))
             self.skip_rows = self.n_leaf
 
-    def step(self, temperature: float, noise):
-        """One optimisation step; returns the (device) loss before the update."""
+    def step(self, temperature: float, noise, next_temperature=None):
+        """One optimisation step; returns the (device) loss before the update.
+
+        ``next_temperature``: the temperature the following ``step`` will be
+        called with (default: the same).  Without clipping the Adam kernel
+        then also writes that step's S rows (update_seq folded into the
+        update, ``trex_adam_seq_update_step``); a following call with a
+        different temperature recomputes them, so the hint only affects
+        speed, never results."""
         L_ = lib()
         st = stream_handle(self.S.device)
         T = float(temperature)
         p = self.params
         N, K = self.N, self.K
-        check(L_.trex_tree_update_seq(ptr(p["ancestors"]), self.n_anc, self.L, self.Q, T,
-                                      ptr(self.S[self.n_leaf:]), st))
+        if self._s_temperature != T:
+            check(L_.trex_tree_update_seq(ptr(p["ancestors"]), self.n_anc, self.L, self.Q, T,
+                                          ptr(self.S[self.n_leaf:]), st))
+        self._s_temperature = None
         check(L_.trex_tree_update_tree(ptr(p["tree_params"]), ptr(noise), None, N, self.n_anc,
                                        1.0, ptr(self.A), st))
         if self.gemm == "x3":
@@ -385,11 +395,15 @@ class TreeOptimizer:
                                     ptr(o.mu["tree_params"]), ptr(o.nu["tree_params"]),
                                     p["tree_params"].numel(), o.count, float(o.lr), float(o.b1),
                                     float(o.b2), float(o.eps), None, 0, 0.0, st))
-            check(L_.trex_adam_seq_step(ptr(self.S[self.n_leaf:]), ptr(self.dS[self.n_leaf:]),
-                                        self.n_anc, self.L, self.Q, T, ptr(p["ancestors"]),
-                                        ptr(o.mu["ancestors"]), ptr(o.nu["ancestors"]), o.count,
-                                        float(o.lr), float(o.b1), float(o.b2), float(o.eps),
-                                        None, st))
+            # ... and update_seq of the next step folded in (S rows rewritten
+            # in place from the new logits)
+            Tn = T if next_temperature is None else float(next_temperature)
+            check(L_.trex_adam_seq_update_step(ptr(self.dS[self.n_leaf:]), self.n_anc, self.L,
+                                               self.Q, T, Tn, ptr(p["ancestors"]),
+                                               ptr(o.mu["ancestors"]), ptr(o.nu["ancestors"]),
+                                               o.count, float(o.lr), float(o.b1), float(o.b2),
+                                               float(o.eps), ptr(self.S[self.n_leaf:]), st))
+            self._s_temperature = Tn
         else:
             check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]),
                                               ptr(self.dS[self.n_leaf:]), self.n_anc, self.L,
