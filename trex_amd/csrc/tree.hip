@@ -21,6 +21,10 @@
 #include "sankoff_dev.h"
 #include "trex_common.h"
 
+#ifndef TREX_MF_DIAG
+#define TREX_MF_DIAG 0
+#endif
+
 namespace trex {
 namespace {
 
@@ -889,6 +893,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
   auto stage = [&](unsigned char* buf, const FSet& f) {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#if TREX_MF_DIAG == 2  // no F split: raw halves (diagnostic, wrong results)
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+      if (!fok[j]) continue;
+      const uint32_t a[4] = {f.a[j].x, f.a[j].y, f.a[j].z, f.a[j].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        unsigned char* col = buf + lofs[j] + c * kMfStride;
+        *reinterpret_cast<uint32_t*>(col) = a[c];
+        *reinterpret_cast<uint32_t*>(col + 64) = a[c] ^ f.b[j].x;
+      }
+    }
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
       if (!fok[j]) continue;
@@ -915,13 +933,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int j = 0; j < 8; ++j)
         mv[j] = (s * 32 + kk * 16 + 8 * h + j < N) ? __uint_as_float(e[j]) : 0.0f;
       h8 ah, al;
+#if TREX_MF_DIAG == 3  // no M split: raw bits as f16 (diagnostic, wrong results)
+      ah = __builtin_bit_cast(h8, w0);
+      al = __builtin_bit_cast(h8, w1);
+      (void)mv;
+#else
       split_h8(mv, sm, ah, al);
+#endif
       const unsigned char* pb = buf + r * kMfStride + kk * 32 + 16 * h;
 #pragma unroll
       for (int t = 0; t < TPC; ++t) {
         const h8 bh = *reinterpret_cast<const h8*>(pb + t * 32 * kMfStride);
         const h8 bl = *reinterpret_cast<const h8*>(pb + t * 32 * kMfStride + 64);
+#if TREX_MF_DIAG == 1  // no MFMA (diagnostic)
+        acc[t][0] += (float)bh[0] + (float)bl[1] + (float)ah[2] + (float)al[3];
+#else
         acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
+#endif
       }
     }
   };
