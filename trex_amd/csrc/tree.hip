@@ -838,22 +838,23 @@ constexpr int kMfStride = 144;
 template <int TPC>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void mf_kernel3(
     const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
-    float* __restrict__ out, float sm, float sf) {
+    int nchunks, float* __restrict__ out, float sm, float sf) {
   constexpr int CW = TPC * 32;
   constexpr int NIT = 16 * (CW / 4);  // (row pair, column group) items per stage
   constexpr int IPT = (NIT + 511) / 512;
   constexpr int BUF = CW * kMfStride;
   extern __shared__ __attribute__((aligned(16))) unsigned char ldsm[];
-  const int c0 = blockIdx.x * CW;
+  const int gx = gridDim.x;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int orow = blockIdx.y * 256 + wave * 32 + r;  // this lane's output row (A fragment row)
+  const int rbase = blockIdx.y * 256 + wave * 32;
+  const int orow = rbase + r;  // this lane's output row (A fragment row)
   const rsrc_t rm = make_rsrc(Mm, (uint32_t)((size_t)N * N * 4));
   const rsrc_t rf = make_rsrc(F, (uint32_t)((size_t)N * K * 4));
   // sentinel leaves room for the small per-load additions below (no int wrap)
   const int mvo = orow < nrows ? ((row0 + orow) * N + 8 * h) * 4 : 0x7FFF0000;
-  int fvo[IPT], lofs[IPT];
+  int fvb[IPT], lofs[IPT];
   bool fok[IPT];
 #pragma unroll
   for (int j = 0; j < IPT; ++j) {
@@ -863,10 +864,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // dwords (conflict-free; cg fastest was a 16-way bank conflict), and
     // read 64 contiguous bytes per F row
     const int p = fok[j] ? item % 16 : 0, cg = fok[j] ? item / 16 : 0;
-    fvo[j] = ((2 * p) * K + c0 + 4 * cg) * 4;
+    fvb[j] = ((2 * p) * K + 4 * cg) * 4;
     lofs[j] = 4 * cg * kMfStride + 4 * p;
   }
   const int nst = (N + 31) / 32;
+  // persistent: this workgroup's column chunks are blockIdx.x + i * gx; the
+  // load pipeline runs straight across chunk boundaries (the next chunk's
+  // first stages are in flight while this one's last stage computes and
+  // its output tile is stored)
+  const int cnt = blockIdx.x < nchunks ? (nchunks - 1 - (int)blockIdx.x) / gx + 1 : 0;
+  const int G = cnt * nst;
 
   f32x16 acc[TPC];
 #pragma unroll
@@ -876,20 +883,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   struct MSet { u32x4 m[4]; };
   FSet f0, f1;
   MSet m0, m1;
-  auto fload = [&](int s, FSet& f) {
-    const int so = s * 32 * K * 4;
+  int fc = blockIdx.x, fs = 0;  // F load cursor (chunk, stage)
+  int ms = 0;                   // M load cursor (stage)
+  int cc = blockIdx.x, cs = 0;  // compute cursor
+  auto fload = [&](FSet& f) {
+    const int so = (fc * CW + fs * 32 * K) * 4;
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
-      const int vo = fok[j] ? fvo[j] + so : 0x7FFF0000;
+      const int vo = fok[j] ? fvb[j] + so : 0x7FFF0000;
       f.a[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, vo, 0, 0);
       f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, fok[j] ? vo + K * 4 : vo, 0, 0);
     }
+    if (++fs == nst) { fs = 0; fc += gx; }
   };
-  auto mload = [&](int s, MSet& m) {
-    const int vo = mvo == 0x7FFF0000 ? mvo : mvo + s * 128;
+  auto mload = [&](MSet& m) {
+    const int vo = mvo == 0x7FFF0000 ? mvo : mvo + ms * 128;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
       m.m[kk] = __builtin_amdgcn_raw_buffer_load_b128(rm, vo + (kk >> 1) * 64 + (kk & 1) * 16, 0, 0);
+    if (++ms == nst) ms = 0;
   };
   auto stage = [&](unsigned char* buf, const FSet& f) {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -923,7 +935,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
   };
-  auto compute = [&](const unsigned char* buf, int s, const MSet& m) {
+  const float unscale = 1.0f / (sm * sf);
+  auto compute = [&](const unsigned char* buf, const MSet& m) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const u32x4 w0 = m.m[2 * kk], w1 = m.m[2 * kk + 1];
@@ -931,7 +944,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       float mv[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        mv[j] = (s * 32 + kk * 16 + 8 * h + j < N) ? __uint_as_float(e[j]) : 0.0f;
+        mv[j] = (cs * 32 + kk * 16 + 8 * h + j < N) ? __uint_as_float(e[j]) : 0.0f;
       h8 ah, al;
 #if TREX_MF_DIAG == 3  // no M split: raw bits as f16 (diagnostic, wrong results)
       ah = __builtin_bit_cast(h8, w0);
@@ -952,42 +965,48 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #endif
       }
     }
+    if (++cs == nst) {  // chunk done: store its tile, restart the accumulators
+      if (rbase < nrows) {
+#pragma unroll
+        for (int t = 0; t < TPC; ++t) {
+          const int col = cc * CW + t * 32 + r;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int row = rbase + (q & 3) + 8 * (q >> 2) + 4 * h;
+            if (row < nrows && col < K) out[(size_t)row * K + col] = acc[t][q] * unscale;
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < TPC; ++t) acc[t] = (f32x16){};
+      cs = 0;
+      cc += gx;
+    }
   };
 
+  if (G == 0) return;
   unsigned char* buf0 = ldsm;
   unsigned char* buf1 = ldsm + BUF;
   // issue order F(0) M(0) F(1) M(1) F(2) ..., i.e. M(x) before F(x + 1)
-  fload(0, f0);
-  mload(0, m0);
-  fload(1, f1);
+  fload(f0);
+  mload(m0);
+  fload(f1);
   stage(buf0, f0);
-  mload(1, m1);
-  fload(2, f0);
+  mload(m1);
+  fload(f0);
   lds_barrier();
-  for (int s = 0; s < nst; s += 2) {
-    compute(buf0, s, m0);
-    if (s + 1 < nst) stage(buf1, f1);
-    mload(s + 2, m0);
-    fload(s + 3, f1);
+  for (int g = 0; g < G; g += 2) {
+    compute(buf0, m0);
+    if (g + 1 < G) stage(buf1, f1);
+    mload(m0);
+    fload(f1);
     lds_barrier();
-    if (s + 1 >= nst) break;
-    compute(buf1, s + 1, m1);
-    if (s + 2 < nst) stage(buf0, f0);
-    mload(s + 3, m1);
-    fload(s + 4, f0);
+    if (g + 1 >= G) break;
+    compute(buf1, m1);
+    if (g + 2 < G) stage(buf0, f0);
+    mload(m1);
+    fload(f0);
     lds_barrier();
-  }
-
-  const float unscale = 1.0f / (sm * sf);
-  if (blockIdx.y * 256 + wave * 32 >= nrows) return;
-#pragma unroll
-  for (int t = 0; t < TPC; ++t) {
-    const int col = c0 + t * 32 + r;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int row = blockIdx.y * 256 + wave * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      if (row < nrows && col < K) out[(size_t)row * K + col] = acc[t][q] * unscale;
-    }
   }
 }
 
@@ -1841,9 +1860,12 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
       if (lds > 65536)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      hipLaunchKernelGGL(kernel, dim3((unsigned)((ct + tpc - 1) / tpc), rg), dim3(512), lds,
-                         (hipStream_t)stream, M, S, N, (int)K, row0, nrows, dS_rows,
-                         split_scale(max_abs_m), split_scale(max_abs_s));
+      const int nch = (int)((ct + tpc - 1) / tpc);
+      // one persistent workgroup per CU (per row group)
+      const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
+      hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(512), lds, (hipStream_t)stream, M, S, N,
+                         (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
+                         split_scale(max_abs_s));
     };
     if (best == 5) go(mf_kernel3<5>, 5);
     else go(mf_kernel3<4>, 4);
