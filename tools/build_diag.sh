@@ -1,6 +1,8 @@
 #!/bin/bash
 # Build libtrexhip variants with a compile-time diagnostic switch in tree.hip:
-#   tools/build_diag.sh NAME "-DTREX_MF_DIAG=1"  ->  trex_amd/NAME.so
+#   tools/build_diag.sh NAME "-DSOME_SWITCH=1"  ->  trex_amd/NAME.so
+# (the TREX_MF_DIAG switches of the first LDS-staged MF, commit 25a91b1,
+# produced the DESIGN.md 5.3 numbers)
 set -e
 cd "$(dirname "$0")/../trex_amd/csrc"
 mkdir -p build/diag

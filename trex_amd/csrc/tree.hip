@@ -21,9 +21,6 @@
 #include "sankoff_dev.h"
 #include "trex_common.h"
 
-#ifndef TREX_MF_DIAG
-#define TREX_MF_DIAG 0
-#endif
 
 namespace trex {
 namespace {
@@ -816,62 +813,87 @@ __global__ __launch_bounds__(kWave) void mf_kernel2(const float* __restrict__ Mm
       }
 }
 
-// ---- v3 MF: out = M[row0 : row0 + nrows] F, LDS-staged F slices ----------
-// A workgroup (8 waves, two per SIMD) owns TPC x 32 output columns and up to
-// 256 output rows (wave w: rows 32w .. 32w + 31 x all TPC column tiles).
-// It walks n in stages of 32 (two 32x32x16 k-steps): the F slice
-// F[n .. n+32)[columns] is loaded ONCE per workgroup from HBM (item (p, cg):
-// rows 2p, 2p + 1, columns 4cg .. 4cg + 3; 64 B runs per row), split into f16 hi /
-// lo and stored column-major in LDS (column stride 144 B: hi n0..31 | lo
-// n0..31 | pad; two n per 32-bit write), so every B fragment is one
-// ds_read_b128; each wave's M fragment (its 32 rows, L2 resident) is loaded
-// directly and split in registers.  Pipeline: F of stages s+1 and s+2 and M
-// of s+1 are in flight while stage s computes (two register sets, loop
-// unrolled by two, loads issued M(x) then F(x+1) so the in-order vmcnt wait
-// for one never waits for the other); LDS double-buffered, one barrier per
-// stage.  All offsets are in voffset, so rows / n past N read out of bounds
-// (0).  TPC is picked per launch so the column tiles divide evenly over the
-// CUs (C5: 6 250 tiles -> 1 250 workgroups of 5 = 5 rounds of 256).  The v2
-// kernel issued one 4-byte load per F element per wave: load-bound.
+// M row-major LDS image stride (bytes): hi n0..31 | lo n0..31 | pad
 constexpr int kMfStride = 144;
 
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+// two ds_read_b64_tr_b16 (rows k .. k+3 and k+4 .. k+7 of one 16-lane
+// group's block) -> the 8-half B fragment of a 32x32x16 f16 MFMA
+__device__ __forceinline__ h8 tr_pair(const unsigned char* p, int four_rows) {
+  typedef __attribute__((address_space(3))) fp16x4_t lds_h4;
+  const fp16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_h4*)(p));
+  const fp16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_h4*)(p + four_rows));
+  const h4 x = __builtin_bit_cast(h4, a), y = __builtin_bit_cast(h4, b);
+  return (h8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+}
+
+// ---- v3 MF: out = M[row0 : row0 + nrows] F, LDS-staged, persistent --------
+// A workgroup (8 waves, two per SIMD) owns TPC x 32 output columns per chunk
+// and up to 256 output rows (wave w: rows 32w .. 32w + 31 x all TPC column
+// tiles); persistent workgroups (one per CU) walk the column chunks
+// blockIdx.x + i * gridDim.x with the load pipeline running straight across
+// chunk boundaries, so one chunk's output stores overlap the next chunk's
+// first loads.  n advances in stages of 32 (two 32x32x16 k-steps).  Per
+// stage both operands are fetched ONCE per workgroup in full 128-B lines and
+// split once into f16 hi / lo:
+//   * F[n .. n+32)[chunk columns] (thread item (n, cg): F[n][4cg .. +3],
+//     column groups fastest) -> ROW-major LDS planes [32 n][CW] (row stride
+//     SF = CW * 2 rounded to 64 mod 256 bytes: conflict-free ds_write_b64
+//     and transposed reads); a B fragment (8 n of one column) is two
+//     ds_read_b64_tr_b16 per plane (gfx950's transposing LDS read: lane
+//     4q+p of a 16-lane group addresses row q, columns 4p..4p+3; lane i
+//     receives column i of the 4 rows);
+//   * M[rows][n .. n+32) (thread t: row t / 8 + 64 i, n segment t % 8) ->
+//     row-major LDS [256][144 B]; an A fragment is one ds_read_b128 per
+//     plane.
+// Two register sets (stages s+1, s+2 in flight), LDS double-buffered, one
+// barrier per stage that waits on lgkmcnt only (__syncthreads() would drain
+// the prefetch).  All offsets are in voffset: rows / n past N read out of
+// bounds (0).  TPC (5 or 4) is picked per launch so column tiles divide
+// evenly over the CUs (C5: 1 250 chunks of 5 tiles over 256 workgroups).
+// Earlier versions (same box, tools/time_gemm.py): v2 (one wave per 64x64
+// tile, operands from L2) 386 us; F staged column-major with 64-B row pieces
+// per load + M fragments loaded per lane 320 us; + M staged in full lines
+// 296 us; this 274 us.
 template <int TPC>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void mf_kernel3(
     const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
     int nchunks, float* __restrict__ out, float sm, float sf) {
   constexpr int CW = TPC * 32;
-  constexpr int NIT = 16 * (CW / 4);  // (row pair, column group) items per stage
+  constexpr int NIT = 32 * (CW / 4);  // F (row, column group) float4 items per stage
   constexpr int IPT = (NIT + 511) / 512;
-  constexpr int BUF = CW * kMfStride;
+  constexpr int SF = (CW * 2 + 191) / 256 * 256 + 64;  // plane row stride (bytes)
+  constexpr int FPLANE = 32 * SF;
+  constexpr int FBUF = 2 * FPLANE;
+  constexpr int MBUF = 256 * kMfStride;
+  constexpr int BUF = FBUF + MBUF;
   extern __shared__ __attribute__((aligned(16))) unsigned char ldsm[];
   const int gx = gridDim.x;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
   const int rbase = blockIdx.y * 256 + wave * 32;
-  const int orow = rbase + r;  // this lane's output row (A fragment row)
   const rsrc_t rm = make_rsrc(Mm, (uint32_t)((size_t)N * N * 4));
   const rsrc_t rf = make_rsrc(F, (uint32_t)((size_t)N * K * 4));
-  // sentinel leaves room for the small per-load additions below (no int wrap)
-  const int mvo = orow < nrows ? ((row0 + orow) * N + 8 * h) * 4 : 0x7FFF0000;
   int fvb[IPT], lofs[IPT];
   bool fok[IPT];
 #pragma unroll
   for (int j = 0; j < IPT; ++j) {
     const int item = tid + 512 * j;
     fok[j] = item < NIT;
-    // p fastest: the 16 lanes of one column group write 16 consecutive LDS
-    // dwords (conflict-free; cg fastest was a 16-way bank conflict), and
-    // read 64 contiguous bytes per F row
-    const int p = fok[j] ? item % 16 : 0, cg = fok[j] ? item / 16 : 0;
-    fvb[j] = ((2 * p) * K + 4 * cg) * 4;
-    lofs[j] = 4 * cg * kMfStride + 4 * p;
+    const int n = fok[j] ? item / (CW / 4) : 0, cg = fok[j] ? item % (CW / 4) : 0;
+    fvb[j] = (n * K + 4 * cg) * 4;
+    lofs[j] = n * SF + 8 * cg;
+  }
+  // M staging: thread t covers rows t / 8 + 64 i (i < 4), n segment t % 8
+  const int mseg = tid & 7, mrow = tid >> 3;
+  int mvb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rg = blockIdx.y * 256 + mrow + 64 * i;
+    mvb[i] = rg < nrows ? ((row0 + rg) * N + 4 * mseg) * 4 : -1;
   }
   const int nst = (N + 31) / 32;
-  // persistent: this workgroup's column chunks are blockIdx.x + i * gx; the
-  // load pipeline runs straight across chunk boundaries (the next chunk's
-  // first stages are in flight while this one's last stage computes and
-  // its output tile is stored)
   const int cnt = blockIdx.x < nchunks ? (nchunks - 1 - (int)blockIdx.x) / gx + 1 : 0;
   const int G = cnt * nst;
 
@@ -879,90 +901,72 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int t = 0; t < TPC; ++t) acc[t] = (f32x16){};
 
-  struct FSet { u32x4 a[IPT], b[IPT]; };
-  struct MSet { u32x4 m[4]; };
-  FSet f0, f1;
-  MSet m0, m1;
-  int fc = blockIdx.x, fs = 0;  // F load cursor (chunk, stage)
-  int ms = 0;                   // M load cursor (stage)
+  struct Set { u32x4 a[IPT], m[4]; int s; };
+  Set r0, r1;
+  int fc = blockIdx.x, fs = 0;  // load cursor (chunk, stage)
   int cc = blockIdx.x, cs = 0;  // compute cursor
-  auto fload = [&](FSet& f) {
+  auto load = [&](Set& q) {
     const int so = (fc * CW + fs * 32 * K) * 4;
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
       const int vo = fok[j] ? fvb[j] + so : 0x7FFF0000;
-      f.a[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, vo, 0, 0);
-      f.b[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, fok[j] ? vo + K * 4 : vo, 0, 0);
+      q.a[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, vo, 0, 0);
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      q.m[i] = __builtin_amdgcn_raw_buffer_load_b128(rm, mvb[i] < 0 ? 0x7FFF0000 : mvb[i] + fs * 128,
+                                                     0, 0);
+    q.s = fs;
     if (++fs == nst) { fs = 0; fc += gx; }
   };
-  auto mload = [&](MSet& m) {
-    const int vo = mvo == 0x7FFF0000 ? mvo : mvo + ms * 128;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-      m.m[kk] = __builtin_amdgcn_raw_buffer_load_b128(rm, vo + (kk >> 1) * 64 + (kk & 1) * 16, 0, 0);
-    if (++ms == nst) ms = 0;
-  };
-  auto stage = [&](unsigned char* buf, const FSet& f) {
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-#if TREX_MF_DIAG == 2  // no F split: raw halves (diagnostic, wrong results)
+  auto stage = [&](unsigned char* buf, const Set& q) {
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
       if (!fok[j]) continue;
-      const uint32_t a[4] = {f.a[j].x, f.a[j].y, f.a[j].z, f.a[j].w};
+      const uint32_t e[4] = {q.a[j].x, q.a[j].y, q.a[j].z, q.a[j].w};
+      h4 hi, lo;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        unsigned char* col = buf + lofs[j] + c * kMfStride;
-        *reinterpret_cast<uint32_t*>(col) = a[c];
-        *reinterpret_cast<uint32_t*>(col + 64) = a[c] ^ f.b[j].x;
+        const float v = __uint_as_float(e[c]) * sf;
+        hi[c] = (_Float16)v;
+        lo[c] = (_Float16)(v - (float)hi[c]);
       }
+      *reinterpret_cast<h4*>(buf + lofs[j]) = hi;
+      *reinterpret_cast<h4*>(buf + FPLANE + lofs[j]) = lo;
     }
-    return;
-#endif
+    unsigned char* mb = buf + FBUF;
 #pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-      if (!fok[j]) continue;
-      const uint32_t a[4] = {f.a[j].x, f.a[j].y, f.a[j].z, f.a[j].w};
-      const uint32_t b[4] = {f.b[j].x, f.b[j].y, f.b[j].z, f.b[j].w};
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t e[4] = {q.m[i].x, q.m[i].y, q.m[i].z, q.m[i].w};
+      h4 hi, lo;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float va = __uint_as_float(a[c]) * sf, vb = __uint_as_float(b[c]) * sf;
-        const _Float16 ha = (_Float16)va, hb = (_Float16)vb;
-        const _Float16 la = (_Float16)(va - (float)ha), lb = (_Float16)(vb - (float)hb);
-        unsigned char* col = buf + lofs[j] + c * kMfStride;
-        *reinterpret_cast<h2*>(col) = (h2){ha, hb};
-        *reinterpret_cast<h2*>(col + 64) = (h2){la, lb};
+        const float v = (q.s * 32 + 4 * mseg + c < N) ? __uint_as_float(e[c]) * sm : 0.0f;
+        hi[c] = (_Float16)v;
+        lo[c] = (_Float16)(v - (float)hi[c]);
       }
+      unsigned char* row = mb + (mrow + 64 * i) * kMfStride + 8 * mseg;
+      *reinterpret_cast<h4*>(row) = hi;
+      *reinterpret_cast<h4*>(row + 64) = lo;
     }
   };
+  // transposed-read lane address: group g = lane / 16, lane 4q + p of it
+  // addresses row 8 (g / 2) + q, columns 16 (g % 2) + 4p .. + 3
+  const int trk = 8 * (lane >> 5) + ((lane & 15) >> 2);
+  const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
   const float unscale = 1.0f / (sm * sf);
-  auto compute = [&](const unsigned char* buf, const MSet& m) {
+  auto compute = [&](const unsigned char* buf) {
+    const unsigned char* pa = buf + FBUF + (wave * 32 + r) * kMfStride + 16 * h;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      const u32x4 w0 = m.m[2 * kk], w1 = m.m[2 * kk + 1];
-      const uint32_t e[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      float mv[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        mv[j] = (cs * 32 + kk * 16 + 8 * h + j < N) ? __uint_as_float(e[j]) : 0.0f;
-      h8 ah, al;
-#if TREX_MF_DIAG == 3  // no M split: raw bits as f16 (diagnostic, wrong results)
-      ah = __builtin_bit_cast(h8, w0);
-      al = __builtin_bit_cast(h8, w1);
-      (void)mv;
-#else
-      split_h8(mv, sm, ah, al);
-#endif
-      const unsigned char* pb = buf + r * kMfStride + kk * 32 + 16 * h;
+      const h8 ah = *reinterpret_cast<const h8*>(pa + kk * 32);
+      const h8 al = *reinterpret_cast<const h8*>(pa + kk * 32 + 64);
 #pragma unroll
       for (int t = 0; t < TPC; ++t) {
-        const h8 bh = *reinterpret_cast<const h8*>(pb + t * 32 * kMfStride);
-        const h8 bl = *reinterpret_cast<const h8*>(pb + t * 32 * kMfStride + 64);
-#if TREX_MF_DIAG == 1  // no MFMA (diagnostic)
-        acc[t][0] += (float)bh[0] + (float)bl[1] + (float)ah[2] + (float)al[3];
-#else
+        const int o1 = (kk * 16 + trk) * SF + (t * 32 + trc) * 2;
+        const h8 bh = tr_pair(buf + o1, 4 * SF);
+        const h8 bl = tr_pair(buf + FPLANE + o1, 4 * SF);
         acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
-#endif
       }
     }
     if (++cs == nst) {  // chunk done: store its tile, restart the accumulators
@@ -987,25 +991,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (G == 0) return;
   unsigned char* buf0 = ldsm;
   unsigned char* buf1 = ldsm + BUF;
-  // issue order F(0) M(0) F(1) M(1) F(2) ..., i.e. M(x) before F(x + 1)
-  fload(f0);
-  mload(m0);
-  fload(f1);
-  stage(buf0, f0);
-  mload(m1);
-  fload(f0);
+  load(r0);
+  load(r1);
+  stage(buf0, r0);
+  load(r0);
   lds_barrier();
   for (int g = 0; g < G; g += 2) {
-    compute(buf0, m0);
-    if (g + 1 < G) stage(buf1, f1);
-    mload(m0);
-    fload(f1);
+    compute(buf0);
+    if (g + 1 < G) stage(buf1, r1);
+    load(r1);
     lds_barrier();
     if (g + 1 >= G) break;
-    compute(buf1, m1);
-    if (g + 2 < G) stage(buf0, f0);
-    mload(m1);
-    fload(f0);
+    compute(buf1);
+    if (g + 2 < G) stage(buf0, r0);
+    load(r0);
     lds_barrier();
   }
 }
@@ -1855,8 +1854,7 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
       const int64_t cost = (wgs + cu_count() - 1) / cu_count() * tpc;
       if (cost < best_cost) { best_cost = cost; best = tpc; }
     }
-    auto go = [&](auto kernel, int tpc) {
-      const int lds = 2 * tpc * 32 * kMfStride;
+    auto go = [&](auto kernel, int tpc, int lds) {
       if (lds > 65536)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1867,8 +1865,8 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
                          (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
                          split_scale(max_abs_s));
     };
-    if (best == 5) go(mf_kernel3<5>, 5);
-    else go(mf_kernel3<4>, 4);
+    if (best == 5) go(mf_kernel3<5>, 5, 2 * (2 * 32 * 320 + 256 * kMfStride));
+    else go(mf_kernel3<4>, 4, 2 * (2 * 32 * 320 + 256 * kMfStride));
     return tree_hip_check("trex_tree_mf_rows_x3");
   }
   const int nrowt = (nrows + 63) / 64;
