@@ -211,6 +211,30 @@ def test_tree_optimizer_matches_oracle_loop(device, gemm):
         np.testing.assert_allclose(_n(opt.params[k]), p_ref[k], rtol=5e-5, atol=5e-6)
 
 
+@pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 8192, 128)])
+def test_gram_x3_stays_inside_its_workspace(device, N, K, skip):
+    """The split-K Gram writes its partials only inside
+    trex_tree_workspace_bytes(N, K) (a guard page of canary bytes after the
+    workspace stays untouched) -- for the skipped and un-skipped tile plans,
+    whose split counts differ."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    rng = np.random.default_rng(K + skip)
+    S = _t(rng.random((N, K)), device)
+    nbytes = int(lib().trex_tree_workspace_bytes(N, K))
+    guard = 1 << 20
+    buf = torch.full((nbytes + guard,), 0xA5, dtype=torch.uint8, device=device)
+    G = torch.zeros((N, N), device=device)
+    check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, skip, 1.0, ptr(G), ptr(buf), nbytes,
+                                       stream_handle(torch.device(device))))
+    torch.cuda.synchronize()
+    assert bool(torch.all(buf[nbytes:] == 0xA5))
+    S64 = _n(S).astype(np.float64)
+    t0 = (skip // 64) * 64
+    ref = S64[t0:] @ S64.T
+    np.testing.assert_allclose(_n(G)[t0:], ref, rtol=1e-5, atol=1e-5 * ref.max())
+
+
 @pytest.mark.parametrize("Q", [4, 5])
 def test_tree_optimizer_next_temperature_hint_is_bitwise_neutral(device, Q):
     """update_seq folded into the Adam kernel (trex_adam_seq_update_step,
