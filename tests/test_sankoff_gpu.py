@@ -26,6 +26,19 @@ pytestmark = pytest.mark.gpu
 SOFT_RTOL = 1e-5
 
 
+@pytest.fixture(autouse=True, params=["lane-per-site", "auto"])
+def q4_kernel(request, monkeypatch):
+    """Every Q <= 4 case runs twice: on the lane-per-site kernel (the C4
+    headline path) and under the library's policy, which sends grids of at
+    most one 64-site wave per CU to the state-parallel kernel (4 lanes per
+    site; sankoff.hip wide_small_q)."""
+    if request.param == "lane-per-site":
+        monkeypatch.setenv("TREX_WIDE_SMALLQ", "0")
+    else:
+        monkeypatch.delenv("TREX_WIDE_SMALLQ", raising=False)
+    return request.param
+
+
 def _engine(children, L, Q, device):
     return SankoffEngine(TreePlan(children), L, Q, device)
 

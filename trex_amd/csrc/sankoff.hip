@@ -1271,6 +1271,21 @@ void launch_res(bool soft, size_t lds, hipStream_t st, const KArgs& A) {
 }
 
 // common entry: validates, fills KArgs, launches one phase
+// Q <= 4 on a small grid (few trees x few sites: C2 is one tree, 157 waves
+// of 64 sites for 1 024 SIMDs) runs the state-parallel kernel instead: 4
+// lanes per site (one per parent state), 16 sites per wave, 4x the waves and
+// a quarter of the per-lane work on the serial node chain.
+// TREX_WIDE_SMALLQ=0 / 1 forces the choice (A/B).
+bool wide_small_q(int B, int L, int Q) {
+  if (Q > 4) return false;
+  // read per call (tests run both kernels in one process)
+  const char* e = std::getenv("TREX_WIDE_SMALLQ");
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  // at most one 64-site wave per CU on the lane-per-site kernel (measured:
+  // C2 74 -> 71 us; a C4 shard, 10 000 waves, is 2.2x slower state-parallel)
+  return (int64_t)B * ((L + kWave - 1) / kWave) <= 256;
+}
+
 int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const int8_t* leaves,
               const float* cost, int B, int L, int n_all, int Q, float tau, unsigned flags,
               float* dp, float* site_score, float* tree_score, const float* dts, float* d_cost,
@@ -1304,7 +1319,7 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
   if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
-  if (Q > 4) {
+  if (Q > 4 || wide_small_q(B, L, Q)) {
     WideCall c;
     c.phase = phase;
     c.soft = tau > 0.0f;
@@ -1417,7 +1432,9 @@ extern "C" int64_t trex_workspace_bytes(int B, int L, int n_all, int Q) {
   if (B <= 0 || L <= 0 || Q <= 0) return 0;
   if (Q > 4) return wide_workspace_bytes(B, L, Q);
   const int64_t nb = (int64_t)B * tiles_for(L, 1);
-  return counters_bytes(B) + nb * 8 * (1 + (int64_t)Q * Q) + (int64_t)Q * Q * B * 8 + 256;
+  const int64_t narrow = counters_bytes(B) + nb * 8 * (1 + (int64_t)Q * Q) + (int64_t)Q * Q * B * 8 + 256;
+  // small grids may run the state-parallel wide kernel (G = 4): room for both
+  return std::max<int64_t>(narrow, wide_workspace_bytes(B, L, Q));
 }
 
 extern "C" int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream) {

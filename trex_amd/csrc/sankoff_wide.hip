@@ -589,6 +589,7 @@ void launch_wide_g(int phase, bool soft, int grid, size_t lds, hipStream_t st, c
 }  // namespace
 
 int wide_group(int Q) {
+  if (Q <= 4) return 4;
   if (Q <= 8) return 8;
   if (Q <= 16) return 16;
   if (Q <= 20) return 20;
@@ -644,6 +645,7 @@ int wide_run(const char* fn, const WideCall& c) {
   hipStream_t st = (hipStream_t)c.stream;
   const int grid = (int)nb;
   switch (wide_group(c.Q)) {
+    case 4: launch_wide_g<4>(c.phase, c.soft, grid, lds, st, A); break;
     case 8: launch_wide_g<8>(c.phase, c.soft, grid, lds, st, A); break;
     case 16: launch_wide_g<16>(c.phase, c.soft, grid, lds, st, A); break;
     case 20: launch_wide_g<20>(c.phase, c.soft, grid, lds, st, A); break;
