@@ -524,12 +524,21 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
 
 // trex-exact ancestral reconstruction on the site-major table
 // (sankoff.py:166-185, 191-267): one lane per site, C in LDS
+// trex-exact reconstruction for Q > 4 (sankoff.py:166-185, 191-267): one
+// lane per site walks the host-simulated DFS order.  The DP row each step
+// reads does not depend on any state, so the next step's row is loaded while
+// this step's argmin runs (ping-pong registers, loop unrolled by two); the
+// states written so far stay in LDS ([n_int][64] bytes per wave) for the
+// children's parent lookups instead of a global store -> load round trip
+// on the chain.
 __global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __restrict__ bt,
                                                                const float* __restrict__ cost,
                                                                const float* __restrict__ dp,
                                                                int n_int, int L, int Q, int tiles,
                                                                int8_t* __restrict__ anc) {
-  __shared__ float c[32 * 32];
+  extern __shared__ __attribute__((aligned(16))) float bl[];
+  float* c = bl;                                              // [32][32]
+  int8_t* sts = reinterpret_cast<int8_t*>(bl + 32 * 32);      // [n_int][64]
   const int tree = blockIdx.x / tiles;
   const int tile = blockIdx.x - tree * tiles;
   const int lane = threadIdx.x;
@@ -540,31 +549,65 @@ __global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __rest
   const cptr<int> prog = as_const(bt) + (size_t)tree * n_int * 2;
   const float* dpt = dp + (size_t)tree * n_int * L * Q + (size_t)site * Q;
   int8_t* at = anc + (size_t)tree * n_int * L + site;
-  for (int k = 0; k < n_int; ++k) {
+  // rows are 16-B aligned when Q % 4 == 0 (site * Q * 4): dwordx4 loads, a
+  // quarter of the address work of 4-byte loads at an 4Q-byte lane stride
+  const bool vec = (Q & 3) == 0;
+  auto load_row = [&](int k, float (&o)[32]) {
+    const int x = (k < n_int) ? (prog[2 * k] & 0xFFFF) : 0;
+    const float* d = dpt + (size_t)x * L * Q;
+    if (vec) {
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const float4 w = (4 * v < Q) ? reinterpret_cast<const float4*>(d)[v]
+                                     : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        o[4 * v] = w.x;
+        o[4 * v + 1] = w.y;
+        o[4 * v + 2] = w.z;
+        o[4 * v + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) o[j] = (j < Q) ? d[j] : 0.0f;
+    }
+  };
+  auto step = [&](int k, const float (&d)[32]) {
     const int ex = prog[2 * k], ey = prog[2 * k + 1];
     const int x = ex & 0xFFFF;
     const int kind = (ex >> 16) & 0xF;
     int out = 0;
     if (kind != kBtUnreached) {
-      const float* d = dpt + (size_t)x * L * Q;
       const bool sent = kind == kBtSentinel;
       if (kind == kBtRoot) {
         float bv = d[0];
-        for (int j = 1; j < Q; ++j) {
+#pragma unroll
+        for (int j = 1; j < 32; ++j) {
+          if (j >= Q) break;
           const float v = d[j];
           if (v < bv) { bv = v; out = j; }
         }
       } else {
-        const int sp = at[(size_t)ey * L];
+        const int sp = sts[ey * kWave + lane];
         const float* row = c + sp * Q;
         float bv = row[0] + (sent ? kSentinel : d[0]);
-        for (int j = 1; j < Q; ++j) {
+#pragma unroll
+        for (int j = 1; j < 32; ++j) {
+          if (j >= Q) break;
           const float v = row[j] + (sent ? kSentinel : d[j]);
           if (v < bv) { bv = v; out = j; }
         }
       }
     }
+    sts[x * kWave + lane] = (int8_t)out;
     at[(size_t)x * L] = (int8_t)out;
+  };
+  float r0[32], r1[32];
+  load_row(0, r0);
+  for (int k = 0; k < n_int; k += 2) {
+    load_row(k + 1, r1);
+    step(k, r0);
+    if (k + 1 >= n_int) break;
+    load_row(k + 2, r0);
+    step(k + 1, r1);
   }
 }
 
@@ -674,7 +717,13 @@ int partial_reduce(const char* fn, const double* part_tree, const double* part_d
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream) {
   const int tiles = (L + kWave - 1) / kWave;
-  hipLaunchKernelGGL(wide_backtrack_kernel, dim3(B * tiles), dim3(kWave), 0, (hipStream_t)stream,
+  const size_t lds = 32 * 32 * 4 + (size_t)ni * kWave;
+  if (lds > 160 * 1024)
+    return set_error(TREX_E_UNSUPPORTED, "trex_sankoff_backtrack: %d internal nodes", ni);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wide_backtrack_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(wide_backtrack_kernel, dim3(B * tiles), dim3(kWave), lds, (hipStream_t)stream,
                      bt, cost, dp, ni, L, Q, tiles, anc);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)
