@@ -650,69 +650,13 @@ __global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// a9 dF = M F  (M [N][N], F [N][K]) on MFMA f32.  One wave = 64 rows x 64
-// columns of dF; reduction over all N inside.  A operand: M rows via float4
-// (k permutation kb + 4h + t), B operand: F rows kb + 4h + t (coalesced).
-// Column blocks are XCD-grouped: the 8 row tiles of a column block share an
-// XCD, so each F block leaves HBM once.
+// a9 dF = M F  (M [N][N], F [N][K]) on MFMA.  Column blocks are XCD-grouped:
+// the row tiles of a column block share an XCD, so each F block leaves HBM
+// once.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWave) void mf_kernel(const float* __restrict__ Mm,
-                                                  const float* __restrict__ F, int N, int K,
-                                                  int nrowt, int ncolb, float* __restrict__ out) {
-  const int b = blockIdx.x;
-  const int xcd = b & 7, m = b >> 3;
-  const int rt = m % nrowt;
-  const int cb = (m / nrowt) * 8 + xcd;
-  if (cb >= ncolb) return;
-  const int lane = threadIdx.x;
-  const int r = lane & 31, h = lane >> 5;
-  const int c0 = cb * 64;
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int v = 0; v < 2; ++v) acc[u][v] = (f32x16){};
-  for (int nb = 0; nb < N; nb += 8) {
-    float ma[2][4], fb[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int row = rt * 64 + u * 32 + r;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int n = nb + 4 * h + t;
-        ma[u][t] = (row < N && n < N) ? Mm[(size_t)row * N + n] : 0.0f;
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const int col = c0 + v * 32 + r;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int n = nb + 4 * h + t;
-        fb[v][t] = (n < N && col < K) ? F[(size_t)n * K + col] : 0.0f;
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-          acc[u][v] = __builtin_amdgcn_mfma_f32_32x32x2f32(ma[u][t], fb[v][t], acc[u][v], 0, 0, 0);
-  }
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int v = 0; v < 2; ++v)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int row = rt * 64 + u * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        const int col = c0 + v * 32 + r;
-        if (row < N && col < K) out[(size_t)row * K + col] = acc[u][v][q];
-      }
-}
 
-// v2 dF = M F: 16 n per step, next step's operands requested before this
+// v2 dF = M F (the f32-MFMA path; the f16x3 one with TREX_GRAM_V2=1): 16 n
+// per step, next step's operands requested before this
 // step's 32 MFMAs (ping-pong registers, unrolled by two).  Lane (r, h)
 // supplies M[row][nb + 8h + t] and F[nb + 8h + t][col]; rows / n / cols past
 // the edges read a clamped address and contribute 0 (M entry zeroed).
