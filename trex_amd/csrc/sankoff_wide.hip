@@ -58,9 +58,26 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 
-// every lane publishes v; each lane gets the G values of its own group
+template <int K_>
+__device__ __forceinline__ float quad_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), K_ * 0x55, 0xF, 0xF, false));
+}
+
+// every lane publishes v; each lane gets the G values of its own group.
+// G = 4 (Q <= 4 on small grids): the group is a DPP quad -- four quad
+// broadcasts, no LDS round trip
 template <int G>
 __device__ __forceinline__ void xchg(float* x, int lane, int gbase, float v, float (&o)[G]) {
+  if constexpr (G == 4) {
+    (void)x;
+    (void)lane;
+    (void)gbase;
+    o[0] = quad_bcast<0>(v);
+    o[1] = quad_bcast<1>(v);
+    o[2] = quad_bcast<2>(v);
+    o[3] = quad_bcast<3>(v);
+    return;
+  }
   x[lane] = v;
   wave_sync();
 #pragma unroll
