@@ -1281,9 +1281,11 @@ bool wide_small_q(int B, int L, int Q) {
   // read per call (tests run both kernels in one process)
   const char* e = std::getenv("TREX_WIDE_SMALLQ");
   if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-  // at most one 64-site wave per CU on the lane-per-site kernel (measured:
-  // C2 74 -> 71 us; a C4 shard, 10 000 waves, is 2.2x slower state-parallel)
-  return (int64_t)B * ((L + kWave - 1) / kWave) <= 256;
+  // up to ~1.5 64-site waves per CU on the lane-per-site kernel (measured,
+  // 32-taxa trees x 5 000 sites: 158 waves 43.8 -> 40.4 us, 316 waves 46.5
+  // -> 44.9 us, 632 waves 48.2 vs 51.8 us (lane-per-site wins); C2 71 ->
+  // 67 us; a C4 shard, 10 000 waves, is 2.2x slower state-parallel)
+  return (int64_t)B * ((L + kWave - 1) / kWave) <= 384;
 }
 
 int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const int8_t* leaves,
