@@ -150,6 +150,41 @@ int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, const float* c
 int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,
                            int n_all, int Q, float* out, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Raw-table entry points: the reference's own run_dp / vectorized_dp and
+ * backtrack_sankoff_jit on its own table layouts, for callers that hold the
+ * tables (src/trex/sankoff.py:24-97, 191-267; the reference's
+ * tests/test_sankoff.py:31 calls run_dp with a caller-initialised table).
+ * Exact reference semantics including caller-visible quirks (see rundp.hip):
+ * leaf rows keep the caller's values except dp[i, int(seq)] = 0; nodes in
+ * index order; child -1 reads the last row; not-yet-written rows hold the
+ * caller's values; first argmin; jnp NaN rules.  Any Q.
+ *   children  int32 [n_all][2], device: the first two rows with
+ *             adjacency[row, node] == 1, -1 filled (sankoff.py:60; run_dp does
+ *             NOT zero adjacency[-1, -1] -- run_sankoff does, :141)
+ *   seqs      fp32 [n_seq >= (n_all+1)/2][n_codes][L] leaf states (vmapped
+ *             run_dp: n_codes = 1, i.e. the (n, L) sequences; the unmapped
+ *             run_dp with a (n, k) sequence array zeroes k states per leaf)
+ *   dp        fp32 [L][n_all][Q] in/out (VmappedDPTable, utils/types.py:53)
+ *   bt        fp32 [L][n_all][Q][4] in/out (BacktrackingTable, :56)
+ * ---------------------------------------------------------------------- */
+int trex_run_dp(const int32_t* children, int n_all, int L, int Q, const float* seqs,
+                int n_codes, const float* cost, float* dp, float* bt, void* stream);
+
+/* vmap(backtrack_sankoff_jit) over L sites (sankoff.py:166-180, 191-267):
+ *   root_state int32 [L], or NULL: jnp.argmin(dp[:, root_node, :], axis=1)
+ *   read from dp fp32 [L][n_all][Q] (sankoff.py:172; dp may be NULL when
+ *   root_state is given); bt fp32 [L][n_all][Q][4]; out int32 [n_all][L]
+ *   (the reference's out_axes=1); stack_ws >= trex_backtrack_workspace_bytes
+ *   device bytes; status int32 [1] device, OR-ed with 1 when some site's DFS
+ *   did not finish within max_steps pops (the reference would not terminate:
+ *   a cyclic table).  The caller reads status after the stream completes. */
+int64_t trex_backtrack_workspace_bytes(int n_all, int L);
+int trex_backtrack_generic(int root_node, const int32_t* root_state, const float* dp,
+                           const float* bt, int n_all, int n_leaves, int L, int Q, int32_t* out,
+                           void* stack_ws, int64_t stack_bytes, int64_t max_steps, int32_t* status,
+                           void* stream);
+
 /* 1 when the DP / marginal tables for Q states are site-major
  * [B][n_int][L][Q], 0 when they are [B][n_int][Q][L].  Always 1 since
  * trex_version() 4 (kept so bindings written against v3 still work). */

@@ -143,6 +143,65 @@ def backtrack_ref(root_node, root_states, bt, n_all, n_leaves):
     return recon
 
 
+def _f2i(x) -> int:
+    """float -> int32 as XLA's convert: truncation, NaN -> 0, saturating."""
+    x = float(x)
+    if x != x:
+        return 0
+    if x >= 2147483647.0:
+        return 2147483647
+    if x <= -2147483648.0:
+        return -2147483648
+    return int(x)
+
+
+def backtrack_site_exact(root_node, root_state, bt_site, n_all, n_leaves, max_steps=1 << 22):
+    """One site of ``backtrack_sankoff_jit`` (sankoff.py:191-267), restated
+    step by step for ANY backtracking table (per-state child ids allowed):
+
+    * stack = zeros((n_all, 2), int32); stack[0] = (root_node, root_state);
+      ptr = 1 (:212-214); loop while ptr > 0 (:220-223);
+    * pop: (node, state) = stack[ptr-1] -- a traced gather, index clamped to
+      n_all-1 (:232-233);
+    * node >= n_leaves (:257-262): recon[node] = state (scatter, dropped when
+      node >= n_all); child_info = bt[node, state] (gather: negative state
+      wraps once, both indices clamped); the float entries are cast to int32
+      when stored into the int32 stack; stack[ptr-1] and stack[ptr] are
+      overwritten (scatters past n_all dropped); ptr += 1 (:236-251);
+    * otherwise ptr -= 1 (:253-254).
+
+    Returns int32 (n_all,), or raises RuntimeError after max_steps pops (the
+    reference would not terminate).
+    """
+    bt_site = np.asarray(bt_site, dtype=np.float32)
+    Q = bt_site.shape[1]
+    stack = np.zeros((n_all, 2), dtype=np.int64)
+    stack[0] = (root_node, root_state)
+    ptr = 1
+    recon = np.zeros(n_all, dtype=np.int64)
+    steps = 0
+    while ptr > 0:
+        steps += 1
+        if steps > max_steps:
+            raise RuntimeError("backtrack does not terminate")
+        cur = ptr - 1
+        node, state = (int(v) for v in stack[min(cur, n_all - 1)])
+        if node >= n_leaves:
+            if node < n_all:
+                recon[node] = state
+            s = state + Q if state < 0 else state
+            s = min(max(s, 0), Q - 1)
+            info = bt_site[min(node, n_all - 1), s]
+            if cur < n_all:
+                stack[cur] = (_f2i(info[0]), _f2i(info[1]))
+            if cur + 1 < n_all:
+                stack[cur + 1] = (_f2i(info[2]), _f2i(info[3]))
+            ptr = cur + 2
+        else:
+            ptr = cur
+    return recon.astype(np.int32)
+
+
 def run_sankoff_ref(adj, cost, seqs, n_all, n_states, n_leaves, return_path=False,
                     dtype=np.float32):
     """``run_sankoff`` (sankoff.py:114-188).  Returns (recon, dp, total)."""

@@ -1,0 +1,58 @@
+"""C-ABI argument validation, callable without a GPU.
+
+The library is compiled with -fno-honor-nans (the kernels drop NaN
+canonicalisation), so its host-side float checks test the IEEE bit pattern
+instead of comparisons the compiler may fold.  Every call below
+is rejected before any launch, so it runs on the CPU container: host numpy
+buffers stand in for device pointers and are never touched.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from trex_amd._lib import TREX_E_ARG, lib
+
+
+def _buf(n=1 << 16):
+    return np.zeros(n, np.uint8)
+
+
+BAD = [float("nan"), float("inf"), -float("inf"), -1.0, -1e-30]
+
+
+@pytest.mark.parametrize("tau", BAD)
+def test_sankoff_rejects_bad_tau(tau):
+    b = _buf()
+    p = b.ctypes.data
+    L = lib()
+    ws = int(L.trex_workspace_bytes(1, 64, 7, 4))
+    w = _buf(ws)
+    rc = L.trex_sankoff_fwd(p, 2, p, p, 1, 64, 7, 4, tau, 0, p, None, p, w.ctypes.data, ws, None)
+    assert rc == TREX_E_ARG, (tau, rc)
+    assert b"tau" in L.trex_last_error()
+    rc = L.trex_sankoff_fwd_bwd(p, 2, p, p, 1, 64, 7, 4, tau, 0, p, None, p, None, p, None, None,
+                                w.ctypes.data, ws, None)
+    assert rc == TREX_E_ARG
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf"), 0.0, -2.0])
+def test_split_gemms_reject_bad_bounds(bad):
+    b = _buf()
+    p = b.ctypes.data
+    L = lib()
+    ws = int(L.trex_tree_workspace_bytes(64, 256))
+    w = _buf(ws)
+    assert L.trex_tree_gram_skip_x3(p, 64, 256, 0, bad, p, w.ctypes.data, ws, None) == TREX_E_ARG
+    assert L.trex_tree_mf_rows_x3(p, p, 64, 256, 0, 64, bad, 1.0, p, None) == TREX_E_ARG
+    assert L.trex_tree_mf_rows_x3(p, p, 64, 256, 0, 64, 65.0, bad, p, None) == TREX_E_ARG
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf"), 0.0, -1.0])
+def test_temperatures_reject_bad_values(bad):
+    b = _buf()
+    p = b.ctypes.data
+    L = lib()
+    assert L.trex_tree_update_tree(p, None, None, 7, 3, bad, p, None) == TREX_E_ARG
+    assert L.trex_tree_update_tree_bwd(p, p, None, 7, 3, bad, p, None) == TREX_E_ARG

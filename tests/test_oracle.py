@@ -145,3 +145,25 @@ def test_golden_fixtures_reproduce():
                                   data[f"{name}/cost"])
         for key, val in res.items():
             np.testing.assert_array_equal(val, data[f"{name}/{key}"], err_msg=f"{name}/{key}")
+
+
+@pytest.mark.parametrize("n_leaves", [8, 6, 10])
+def test_exact_backtrack_restatement_agrees_with_topology_simulation(n_leaves):
+    """oracle.backtrack_site_exact (the reference's stack machine step by
+    step, sankoff.py:212-265) == backtrack_ref (DFS simulated once on the
+    topology) on run_dp's tables, including n_leaves != (n_all+1)//2."""
+    from oracle.sankoff_ref import backtrack_ref, backtrack_site_exact
+
+    ch = random_topologies(1, 8, seed=n_leaves)[0]
+    adj = adjacency_from_children(ch)[0]
+    rng = np.random.default_rng(n_leaves)
+    L, Q = 40, 4
+    seqs = rng.integers(0, Q, size=(8, L)).astype(np.float32)
+    dp0 = np.full((L, 15, Q), 1e5, np.float32)
+    bt0 = np.zeros((L, 15, Q, 4), np.float32)
+    dp, bt = run_dp_ref(adj, dp0, bt0, seqs, int_cost(Q, seed=1))
+    roots = dp[:, -1].argmin(axis=1).astype(np.int32)
+    want = backtrack_ref(14, roots, bt, 15, n_leaves)
+    for l in range(L):
+        np.testing.assert_array_equal(backtrack_site_exact(14, roots[l], bt[l], 15, n_leaves),
+                                      want[:, l])

@@ -26,14 +26,17 @@ pytestmark = pytest.mark.gpu
 SOFT_RTOL = 1e-5
 
 
-@pytest.fixture(autouse=True, params=["lane-per-site", "auto"])
+@pytest.fixture(autouse=True, params=["lane-per-site", "state-parallel", "auto"])
 def q4_kernel(request, monkeypatch):
-    """Every Q <= 4 case runs twice: on the lane-per-site kernel (the C4
-    headline path) and under the library's policy, which sends grids of at
-    most one 64-site wave per CU to the state-parallel kernel (4 lanes per
-    site; sankoff.hip wide_small_q)."""
+    """Every Q <= 4 case runs three times: on the lane-per-site kernel (the
+    C4 headline path), on the state-parallel kernel (4 lanes per site, one
+    DPP quad, G = 4; Q = 2 / 3 pad the quad), and under the library's policy
+    (sankoff.hip wide_small_q: grids of at most ~1.5 64-site waves per CU go
+    state-parallel)."""
     if request.param == "lane-per-site":
         monkeypatch.setenv("TREX_WIDE_SMALLQ", "0")
+    elif request.param == "state-parallel":
+        monkeypatch.setenv("TREX_WIDE_SMALLQ", "1")
     else:
         monkeypatch.delenv("TREX_WIDE_SMALLQ", raising=False)
     return request.param

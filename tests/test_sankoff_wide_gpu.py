@@ -184,9 +184,10 @@ def test_fused_equals_separate_wide(device, tau):
 
 
 def test_c3_scale_properties(device):
-    """C3 shape: 64 taxa x 10 000 sites x 20 states, softmin (tau 0.5) +
-    ancestral reconstruction.  Score and dC vs the fp64 oracle, determinism,
-    tau = 0 ancestral states bit-exact vs the reference backtrack."""
+    """C3 at its stated size: 64 taxa x 10 000 sites x 20 states, softmin
+    (tau 0.5) + ancestral reconstruction.  Score, dC, DP table, marginals and
+    soft ancestral states vs the fp64 oracle; determinism; tau = 0 DP table,
+    total and trex ancestral states bit-exact vs the reference restatement."""
     n, L, Q, tau = 64, 10000, 20, 0.5
     ch = random_topologies(1, n, seed=31)
     leaves = random_leaves(1, n, L, Q, seed=32)
@@ -202,11 +203,23 @@ def test_c3_scale_properties(device):
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL,
                                atol=SOFT_RTOL * np.abs(ref["d_cost"]).max())
-    # hard path + trex backtrack at full size
+    # full-size DP table, marginals and soft ancestral states (the marginal
+    # tolerance rule of tests/test_sankoff_gpu.py: softmax of D / tau in fp32)
+    np.testing.assert_allclose(_sm(f.dp), ref["dp"], rtol=SOFT_RTOL,
+                               atol=SOFT_RTOL * np.abs(ref["dp"]).max())
+    mtol = max(2e-5, 8 * 1.2e-7 * np.abs(ref["dp"]).max() / tau)
+    np.testing.assert_allclose(_sm(mg), ref["marginals"], atol=mtol)
+    m = ref["marginals"]
+    top2 = np.sort(m, axis=2)[:, :, -2:, :]
+    clear = (top2[:, :, 1] - top2[:, :, 0]) > 4 * mtol
+    np.testing.assert_array_equal(an.cpu().numpy()[clear], m.argmax(axis=2)[clear])
+    del ref, m, top2, clear
+    # hard path + trex backtrack at full size: DP table, total, states exact
     h = eng.forward(lv, c, 0.0)
     anc = eng.backtrack(c, h.dp).cpu().numpy()[0]
     adj = adjacency_from_children(ch)[0]
     r = run_sankoff_ref(adj, cost, leaves[0].astype(np.float32), 2 * n - 1, Q, n,
                         return_path=True)
     assert float(h.tree_score[0]) == float(r[2])
+    np.testing.assert_array_equal(h.dp.cpu().numpy()[0], r[1][:, n:, :].transpose(1, 0, 2))
     np.testing.assert_array_equal(anc.astype(np.float32), r[0][n:])

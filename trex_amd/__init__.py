@@ -8,9 +8,13 @@ land, ``trex.tree``) on top of hand-written HIP kernels for gfx950 in
 from ._lib import LIB_PATH, TrexError, lib  # noqa: F401
 from .sankoff import (  # noqa: F401
     SankoffEngine,
+    backtrack_sankoff_jit,
     leaf_codes,
+    run_dp,
     run_sankoff,
     sankoff_value_and_grad,
+    vectorized_dp,
+    vmapped_backtrack,
 )
 from .topology import (  # noqa: F401
     TreePlan,
@@ -20,7 +24,8 @@ from .topology import (  # noqa: F401
 )
 
 __all__ = [
-    "LIB_PATH", "TrexError", "lib", "SankoffEngine", "leaf_codes", "run_sankoff",
+    "LIB_PATH", "TrexError", "lib", "SankoffEngine", "leaf_codes", "run_sankoff", "run_dp",
+    "vectorized_dp", "backtrack_sankoff_jit", "vmapped_backtrack",
     "sankoff_value_and_grad", "TreePlan", "children_from_adjacency",
     "create_balanced_binary_tree", "random_topologies",
 ]

@@ -45,6 +45,11 @@ SIGNATURES = {
     "trex_sankoff_backtrack": (_c_i, [_p, _c_i, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
     "trex_dp_to_trex_layout": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
     "trex_dp_site_major": (_c_i, [_c_i]),
+    # raw-table run_dp / backtrack_sankoff_jit
+    "trex_run_dp": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _c_i, _p, _p, _p, _p]),
+    "trex_backtrack_workspace_bytes": (_c_i64, [_c_i, _c_i]),
+    "trex_backtrack_generic": (_c_i, [_c_i, _p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _c_i64,
+                                      _c_i64, _p, _p]),
     # tree-cost path
     "trex_tree_discretize": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _p]),
     "trex_tree_update_seq": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _p, _p]),

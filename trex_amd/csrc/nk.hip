@@ -610,7 +610,7 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
     return set_error(TREX_E_ARG, "%s: null pointer / bad sizes", fn);
   if (workspace_bytes < trex_nk_workspace_bytes(N, L, Q, k, n_parents))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
-  if (!(n_valid > 0.0f) || n_nonroot <= 0)
+  if (!pos_finite_f32(n_valid) || n_nonroot <= 0)
     return set_error(TREX_E_ARG, "%s: empty normaliser (n_valid=%g, n_nonroot=%d)", fn, n_valid,
                      n_nonroot);
   hipStream_t st = (hipStream_t)stream;

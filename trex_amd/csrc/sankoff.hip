@@ -1150,6 +1150,9 @@ int device_cus() {
   return cus;
 }
 
+// A/B-only path: with the wide_small_q policy every grid this would pick
+// (<= one wave per CU) already runs on the state-parallel kernel, so it is
+// reached only under TREX_WIDE_SMALLQ=0 (the tests' lane-per-site pass).
 // Resident mode trades the adjoint's HBM re-read of the DP table for LDS
 // occupancy.  Measured on the C4 shard (32 taxa, 31 KiB per wave, one wave
 // per SIMD) it is 2.3x slower than the re-reading kernel (410 vs 176 us: a
@@ -1281,11 +1284,12 @@ bool wide_small_q(int B, int L, int Q) {
   // read per call (tests run both kernels in one process)
   const char* e = std::getenv("TREX_WIDE_SMALLQ");
   if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-  // up to ~1.5 64-site waves per CU on the lane-per-site kernel (measured,
-  // 32-taxa trees x 5 000 sites: 158 waves 43.8 -> 40.4 us, 316 waves 46.5
-  // -> 44.9 us, 632 waves 48.2 vs 51.8 us (lane-per-site wins); C2 71 ->
-  // 67 us; a C4 shard, 10 000 waves, is 2.2x slower state-parallel)
-  return (int64_t)B * ((L + kWave - 1) / kWave) <= 384;
+  // up to ~1.5 64-site waves per CU on the lane-per-site kernel (measured
+  // on 256 CUs, 32-taxa trees x 5 000 sites: 158 waves 43.8 -> 40.4 us, 316
+  // waves 46.5 -> 44.9 us, 632 waves 48.2 vs 51.8 us (lane-per-site wins);
+  // C2 71 -> 67 us; a C4 shard, 10 000 waves, is 2.2x slower
+  // state-parallel).  Scaled by the CU count (a CPX partition has 32 CUs).
+  return (int64_t)B * ((L + kWave - 1) / kWave) * 2 <= (int64_t)3 * device_cus();
 }
 
 int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const int8_t* leaves,
@@ -1316,7 +1320,7 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   if ((phase & 1) && !tree_score) return set_error(TREX_E_ARG, "%s: tree_score is required", fn);
   if ((phase & 2) && (!dp || !d_cost))
     return set_error(TREX_E_ARG, "%s: dp and d_cost are required", fn);
-  if (!(tau >= 0.0f) || std::isinf(tau))
+  if (!nonneg_finite_f32(tau))
     return set_error(TREX_E_ARG, "%s: tau must be finite and >= 0 (got %g)", fn, tau);
   if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
@@ -1553,7 +1557,7 @@ extern "C" int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_
     return set_error(TREX_E_ARG, "%s: null pointer argument", fn);
   if ((phase & 1) && !tree_score) return set_error(TREX_E_ARG, "%s: tree_score is required", fn);
   if ((phase & 2) && !d_cost) return set_error(TREX_E_ARG, "%s: d_cost is required", fn);
-  if (!(tau >= 0.0f) || std::isinf(tau))
+  if (!nonneg_finite_f32(tau))
     return set_error(TREX_E_ARG, "%s: tau must be finite and >= 0 (got %g)", fn, tau);
   if (workspace_bytes < trex_ragged_workspace_bytes(items, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);

@@ -1379,7 +1379,7 @@ extern "C" int trex_tree_update_seq_bwd(const float* s, const float* ds, int n_a
 
 extern "C" int trex_tree_update_tree(const float* theta, const float* noise, const float* gates,
                                      int N, int n_anc, float T, float* A, void* stream) {
-  if (!A || N < 2 || n_anc < 0 || n_anc >= N || !(T > 0.0f))
+  if (!A || N < 2 || n_anc < 0 || n_anc >= N || !pos_finite_f32(T))
     return set_error(TREX_E_ARG, "trex_tree_update_tree: bad arguments");
   if (n_anc > 0 && !theta) return set_error(TREX_E_ARG, "trex_tree_update_tree: theta is NULL");
   if (n_anc == 0) {  // tree.py:68-69: identity
@@ -1394,7 +1394,7 @@ extern "C" int trex_tree_update_tree(const float* theta, const float* noise, con
 
 extern "C" int trex_tree_update_tree_bwd(const float* A, const float* dA, const float* gates,
                                          int N, int n_anc, float T, float* dtheta, void* stream) {
-  if (!A || !dA || !dtheta || N < 2 || n_anc <= 0 || n_anc >= N || !(T > 0.0f))
+  if (!A || !dA || !dtheta || N < 2 || n_anc <= 0 || n_anc >= N || !pos_finite_f32(T))
     return set_error(TREX_E_ARG, "trex_tree_update_tree_bwd: bad arguments");
   hipLaunchKernelGGL(update_tree_bwd_kernel, dim3(N - 1), dim3(256), 0, (hipStream_t)stream, A,
                      dA, gates, N, n_anc, T, dtheta);
@@ -1476,7 +1476,7 @@ extern "C" int64_t trex_tree_workspace_bytes(int N, int64_t K) {
 namespace {
 // power of two s with max_abs * s <= 2^14 (f16 split headroom)
 float split_scale(float max_abs) {
-  if (!(max_abs > 0.0f)) return 1.0f;
+  if (!pos_finite_f32(max_abs)) return 1.0f;
   return std::ldexp(1.0f, 14 - (int)std::ceil(std::log2((double)max_abs)));
 }
 
@@ -1656,7 +1656,7 @@ extern "C" int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n
                                   int count, float lr, float b1, float b2, float eps,
                                   float* grads_out, void* stream) {
   if (!s_anc || !ds_anc || !params || !mu || !nu || n_anc <= 0 || L <= 0 || Q < 2 || Q > 32 ||
-      count < 1 || !(temperature > 0.0f))
+      count < 1 || !pos_finite_f32(temperature))
     return set_error(TREX_E_ARG, "trex_adam_seq_step: bad arguments");
   const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
   const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
@@ -1681,7 +1681,7 @@ extern "C" int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, 
                                          float b1, float b2, float eps, float* s_next,
                                          void* stream) {
   if (!ds_anc || !params || !mu || !nu || !s_next || n_anc <= 0 || L <= 0 || Q < 2 || Q > 32 ||
-      count < 1 || !(temperature > 0.0f) || !(next_temperature > 0.0f))
+      count < 1 || !pos_finite_f32(temperature) || !pos_finite_f32(next_temperature))
     return set_error(TREX_E_ARG, "trex_adam_seq_update_step: bad arguments");
   const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
   const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
@@ -1736,7 +1736,7 @@ extern "C" int trex_tree_gram_skip_x3(const float* S, int N, int64_t K, int skip
                                       float max_abs, float* G, void* workspace,
                                       int64_t workspace_bytes, void* stream) {
   if (!S || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF || skip_rows < 0 ||
-      skip_rows > N || !(max_abs > 0.0f) || std::isinf(max_abs))
+      skip_rows > N || !pos_finite_f32(max_abs))
     return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3: bad arguments");
   if (K % 16 != 0)
     return set_error(TREX_E_UNSUPPORTED, "trex_tree_gram_skip_x3: K = L*Q must be a multiple of 16");
@@ -1782,8 +1782,7 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
                                     int nrows, float max_abs_m, float max_abs_s, float* dS_rows,
                                     void* stream) {
   if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
-      row0 + nrows > N || !(max_abs_m > 0.0f) || !(max_abs_s > 0.0f) || std::isinf(max_abs_m) ||
-      std::isinf(max_abs_s))
+      row0 + nrows > N || !pos_finite_f32(max_abs_m) || !pos_finite_f32(max_abs_s))
     return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3: bad arguments");
   if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
     return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows_x3: S exceeds 2 GiB");

@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
 
 #include "../../include/trex_hip.h"
 
@@ -30,6 +31,26 @@ constexpr int kBtSentinel = 2;
 constexpr int kBtUnreached = 3;
 
 int set_error(int code, const char* fmt, ...);
+
+// Host argument checks on the IEEE bit pattern: the library is compiled with
+// -fno-honor-nans (kernels drop NaN canonicalisation), under which the
+// compiler may fold `!(x >= 0.0f)` or std::isnan(x) to false for a NaN x.
+inline uint32_t float_bits(float x) {
+  uint32_t u;
+  std::memcpy(&u, &x, sizeof u);
+  return u;
+}
+inline bool finite_f32(float x) { return (float_bits(x) & 0x7f800000u) != 0x7f800000u; }
+// finite and >= 0 (-0.0 included)
+inline bool nonneg_finite_f32(float x) {
+  const uint32_t u = float_bits(x);
+  return finite_f32(x) && (!(u >> 31) || (u & 0x7fffffffu) == 0);
+}
+// finite and > 0
+inline bool pos_finite_f32(float x) {
+  const uint32_t u = float_bits(x);
+  return finite_f32(x) && !(u >> 31) && (u & 0x7fffffffu) != 0;
+}
 
 // ---- Q > 4: state-parallel kernels on a site-major DP table (sankoff_wide.hip)
 struct WideCall {

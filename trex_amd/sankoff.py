@@ -18,7 +18,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from ._lib import TREX_FLAG_HARD_ROOT, check, lib, ptr, stream_handle
-from .topology import TreePlan
+from .topology import TreePlan, children_from_adjacency
 
 SENTINEL = 1e5  # src/trex/sankoff.py:152
 
@@ -279,20 +279,20 @@ def _prepare(adjacency_matrix, cost_matrix, sequences, n_all, n_states, n_leaves
     adj = _to_host(adjacency_matrix)
     if adj.shape != (n_all, n_all):
         raise ValueError(f"adjacency_matrix must be ({n_all}, {n_all}), got {adj.shape}")
-    if n_leaves != (n_all + 1) // 2:
-        raise NotImplementedError(
-            "trex's DP initialises (n_all+1)//2 leaf rows (sankoff.py:46); n_leaves must match")
     device = device or _default_device()
     seqs = torch.as_tensor(sequences)
-    if seqs.ndim != 2 or seqs.shape[0] < n_leaves:
-        raise ValueError(f"sequences must be (>= {n_leaves}, L), got {tuple(seqs.shape)}")
+    # the DP reads (n_all+1)//2 leaf rows whatever n_leaves says (sankoff.py:46,49);
+    # run_sankoff copies n_leaves of them into the reconstruction (:162)
+    need = max(n_leaves, (n_all + 1) // 2)
+    if seqs.ndim != 2 or seqs.shape[0] < need:
+        raise ValueError(f"sequences must be (>= {need}, L), got {tuple(seqs.shape)}")
     cost = torch.as_tensor(cost_matrix).to(device=device, dtype=torch.float32).contiguous()
     if tuple(cost.shape) != (n_states, n_states):
         raise ValueError(f"cost_matrix must be ({n_states}, {n_states})")
     plan = _plan_for(adj)
     L = int(seqs.shape[1])
     eng = _engine_for(plan, L, n_states, device)
-    codes = leaf_codes(seqs[:n_leaves], n_states, device)[None].contiguous()
+    codes = leaf_codes(seqs[:(n_all + 1) // 2], n_states, device)[None].contiguous()
     return plan, eng, codes, cost, seqs
 
 
@@ -312,8 +312,23 @@ def run_sankoff(adjacency_matrix, cost_matrix, sequences, n_all: int, n_states: 
     recon = torch.zeros((n_all, L), dtype=torch.float32, device=eng.device)
     recon[:n_leaves] = seqs[:n_leaves].to(device=eng.device, dtype=torch.float32)
     if return_path:
-        anc = eng.backtrack(cost, f.dp)[0]
-        recon[n_leaves:] = anc.to(torch.float32)
+        if n_leaves == (n_all + 1) // 2:
+            anc = eng.backtrack(cost, f.dp)[0]
+            recon[n_leaves:] = anc.to(torch.float32)
+        else:
+            # the reference backtracks with the n_leaves argument while its DP
+            # used (n_all+1)//2 leaf rows (sankoff.py:46 vs :179): rows the
+            # two disagree on follow the raw backtracking table, so take the
+            # raw-table path (run_dp's table, then the reference's DFS)
+            adj = np.array(_to_host(adjacency_matrix), dtype=np.float32, copy=True)
+            adj[-1, -1] = 0
+            _, bt = vectorized_dp(adj, torch.full((L, n_all, n_states), SENTINEL,
+                                                  dtype=torch.float32, device=eng.device),
+                                  torch.zeros((L, n_all, n_states, 4), dtype=torch.float32,
+                                              device=eng.device),
+                                  seqs.to(device=eng.device, dtype=torch.float32), cost)
+            chars = vmapped_backtrack(n_all - 1, None, bt, n_all, n_leaves, dp=dp_trex)
+            recon[n_leaves:] = chars[n_leaves:].to(torch.float32)
     return recon, dp_trex, f.tree_score[0]
 
 
@@ -330,3 +345,137 @@ def sankoff_value_and_grad(adjacency_matrix, cost_matrix, sequences, n_all: int,
                                       n_states, n_leaves, device)
     ts, dc = eng.value_and_grad(codes, cost, tau, hard_root=hard_root)
     return ts[0], dc
+
+
+# ---------------------------------------------------------------------------
+# raw-table entry points: run_dp / vectorized_dp / backtrack_sankoff_jit on the
+# reference's own table layouts (rundp.hip)
+# ---------------------------------------------------------------------------
+def _f32_dev(x, device):
+    torch = _torch()
+    return torch.as_tensor(x).to(device=device, dtype=torch.float32).contiguous()
+
+
+def _raw_dp(adjacency_matrix, dp, bt, seqs3, cost_matrix, device):
+    """dp (L, n_all, Q), bt (L, n_all, Q, 4), seqs3 (n, n_codes, L) -> new (dp, bt)."""
+    torch = _torch()
+    adj = _to_host(adjacency_matrix)
+    if adj.ndim != 2 or adj.shape[0] != adj.shape[1]:
+        raise ValueError(f"adjacency_matrix must be square, got {adj.shape}")
+    n_all = adj.shape[0]
+    L, n2, Q = dp.shape
+    if n2 != n_all or tuple(bt.shape) != (L, n_all, Q, 4):
+        raise ValueError(f"tables must be ({L}, {n_all}, {Q}) and ({L}, {n_all}, {Q}, 4), got "
+                         f"{tuple(dp.shape)} and {tuple(bt.shape)}")
+    nl = (n_all + 1) // 2
+    if seqs3.shape[0] < nl or seqs3.shape[2] != L:
+        raise ValueError(f"sequences need >= {nl} leaf rows over {L} sites")
+    cost = _f32_dev(cost_matrix, device)
+    if tuple(cost.shape) != (Q, Q):
+        raise ValueError(f"cost_matrix must be ({Q}, {Q})")
+    # run_dp does not drop the root self-loop (run_sankoff does, sankoff.py:141)
+    ch = children_from_adjacency(adj, drop_root_self_loop=False)[0]
+    ch_dev = torch.as_tensor(ch, device=device).contiguous()
+    dp_out = _f32_dev(dp, device).clone()
+    bt_out = _f32_dev(bt, device).clone()
+    sq = _f32_dev(seqs3, device)
+    check(lib().trex_run_dp(ptr(ch_dev), n_all, L, Q, ptr(sq), int(sq.shape[1]), ptr(cost),
+                            ptr(dp_out), ptr(bt_out), stream_handle(device)))
+    return dp_out, bt_out
+
+
+def run_dp(adjacency_matrix, dynamic_programming_table, backtracking_table, sequences,
+           cost_matrix, *, device=None):
+    """trex's ``run_dp`` (sankoff.py:24-94) for one site on the device.
+
+    dynamic_programming_table (n_all, Q) and backtracking_table (n_all, Q, 4)
+    as the caller initialised them (inputs are not modified); sequences
+    (n >= (n_all+1)//2,) states, or (n, k): ``.at[i, sequences[i]]`` then
+    zeroes all k listed states of leaf i.  Returns new (dp, bt) tensors.
+    """
+    torch = _torch()
+    device = torch.device(device) if device is not None else _default_device()
+    dp = torch.as_tensor(dynamic_programming_table)
+    bt = torch.as_tensor(backtracking_table)
+    if dp.ndim != 2 or bt.ndim != 3:
+        raise ValueError("run_dp takes one site's (n_all, Q) / (n_all, Q, 4) tables")
+    sq = torch.as_tensor(sequences).to(torch.float32)
+    if sq.ndim == 1:
+        sq = sq[:, None]
+    if sq.ndim != 2:
+        raise ValueError("sequences must be (n,) or (n, k)")
+    d, b = _raw_dp(adjacency_matrix, dp[None], bt[None], sq[:, :, None], cost_matrix, device)
+    return d[0], b[0]
+
+
+def vectorized_dp(adjacency_matrix, dynamic_programming_table, backtracking_table, sequences,
+                  cost_matrix, *, device=None):
+    """``vmap(run_dp, (None, 0, 0, 1, None))`` (sankoff.py:97): tables
+    (L, n_all, Q) / (L, n_all, Q, 4), sequences (n, L).  Returns new tables."""
+    torch = _torch()
+    device = torch.device(device) if device is not None else _default_device()
+    dp = torch.as_tensor(dynamic_programming_table)
+    bt = torch.as_tensor(backtracking_table)
+    sq = torch.as_tensor(sequences)
+    if dp.ndim != 3 or bt.ndim != 4 or sq.ndim != 2:
+        raise ValueError("vectorized_dp takes (L, n_all, Q), (L, n_all, Q, 4), (n, L)")
+    return _raw_dp(adjacency_matrix, dp, bt, sq[:, None, :], cost_matrix, device)
+
+
+_MAX_BACKTRACK_STEPS = 1 << 26
+
+
+def vmapped_backtrack(root_node, root_states, backtracking_table, n_all: int, n_leaves: int, *,
+                      dp=None, device=None):
+    """``vmap(backtrack_sankoff_jit, in_axes=(None, 0, 0, None, None),
+    out_axes=1)`` (sankoff.py:166-180): bt (L, n_all, Q, 4), root_states (L,)
+    -> int32 (n_all, L).  root_states None: first argmin of dp[:, root_node]
+    (dp (L, n_all, Q), sankoff.py:172).  A table whose DFS would not terminate
+    (the reference hangs) raises TrexError(TREX_E_TOPOLOGY)."""
+    from ._lib import TREX_E_TOPOLOGY, TrexError
+
+    torch = _torch()
+    bt = torch.as_tensor(backtracking_table)
+    device = (torch.device(device) if device is not None
+              else (bt.device if bt.is_cuda else _default_device()))
+    bt = _f32_dev(bt, device)
+    if bt.ndim != 4 or bt.shape[1] != n_all or bt.shape[3] != 4:
+        raise ValueError(f"backtracking_table must be (L, {n_all}, Q, 4)")
+    L, _, Q, _ = bt.shape
+    rs = None
+    dpt = None
+    if root_states is not None:
+        rs = torch.as_tensor(root_states).to(device=device, dtype=torch.int32).reshape(-1)
+        if rs.numel() != L:
+            raise ValueError(f"root_states must have {L} entries")
+        rs = rs.contiguous()
+    else:
+        if dp is None:
+            raise ValueError("root_states or dp is required")
+        dpt = _f32_dev(dp, device)
+        if tuple(dpt.shape) != (L, n_all, Q):
+            raise ValueError(f"dp must be ({L}, {n_all}, {Q})")
+    out = torch.empty((n_all, L), dtype=torch.int32, device=device)
+    nbytes = int(lib().trex_backtrack_workspace_bytes(n_all, L))
+    stack = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    check(lib().trex_backtrack_generic(int(root_node), ptr(rs), ptr(dpt), ptr(bt), n_all,
+                                       int(n_leaves), L, Q, ptr(out), ptr(stack), nbytes,
+                                       _MAX_BACKTRACK_STEPS, ptr(status), stream_handle(device)))
+    if int(status.item()) != 0:
+        raise TrexError(TREX_E_TOPOLOGY, "backtrack_sankoff_jit: the DFS over this backtracking "
+                        "table does not terminate (the reference would not return)")
+    return out
+
+
+def backtrack_sankoff_jit(root_node, root_state, backtracking_table, n_all: int, n_leaves: int,
+                          *, device=None):
+    """trex's ``backtrack_sankoff_jit`` (sankoff.py:191-267) for one site:
+    bt (n_all, Q, 4), root_state scalar -> int32 (n_all,) reconstructed states."""
+    torch = _torch()
+    bt = torch.as_tensor(backtracking_table)
+    if bt.ndim != 3:
+        raise ValueError("backtrack_sankoff_jit takes one site's (n_all, Q, 4) table; "
+                         "use vmapped_backtrack for (L, n_all, Q, 4)")
+    rs = torch.as_tensor(root_state).reshape(1)
+    return vmapped_backtrack(root_node, rs, bt[None], n_all, n_leaves, device=device)[:, 0]

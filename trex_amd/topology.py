@@ -12,12 +12,13 @@ import numpy as np
 from ._lib import TREX_PLAN_HEADER_INTS, check, lib
 
 
-def children_from_adjacency(adj) -> np.ndarray:
+def children_from_adjacency(adj, *, drop_root_self_loop: bool = True) -> np.ndarray:
     """trex's child lists for every node.
 
     ``jnp.where(adj[:, node] == 1, size=2, fill_value=-1)[0]``
     (src/trex/sankoff.py:60) applied after run_sankoff zeroes ``adj[-1, -1]``
-    (sankoff.py:141).  ``adj``: (n_all, n_all) or (B, n_all, n_all).
+    (sankoff.py:141; ``drop_root_self_loop=False`` is run_dp called directly,
+    which does not).  ``adj``: (n_all, n_all) or (B, n_all, n_all).
     Returns int32 (B, n_all, 2).
     """
     a = np.asarray(adj)
@@ -26,7 +27,8 @@ def children_from_adjacency(adj) -> np.ndarray:
     if a.ndim != 3 or a.shape[1] != a.shape[2]:
         raise ValueError(f"adjacency must be (n_all, n_all) or (B, n_all, n_all), got {a.shape}")
     mask = a == 1
-    mask[:, -1, -1] = False
+    if drop_root_self_loop:
+        mask[:, -1, -1] = False
     B, n_all, _ = mask.shape
     # cumulative count down each column; first hit has count 1, second count 2
     cnt = np.cumsum(mask, axis=1)
