@@ -384,6 +384,24 @@ int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const float* S, i
                            const float* surrogate, const float* d_S_in, float* loss, float* d_S,
                            void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ========================================================================
+ * Multi-GPU exchange: the sharded paths' only collective
+ * is the sum over ranks of one small fp32 buffer -- [dC, loss] (Q*Q + 1
+ * floats) for the tree-batch-sharded Sankoff step, the N x N Gram for the
+ * site-sharded tree-cost step.  One RCCL all-reduce on the caller's stream.
+ * RCCL is loaded with dlopen on first use (TREX_E_UNSUPPORTED if absent).
+ *   trex_comm_get_unique_id: on one rank; broadcast the bytes to the others
+ *   trex_comm_init: one communicator per (process, device ordinal dev); the
+ *     returned comm is an ncclComm_t -- a caller's own RCCL communicator may
+ *     be passed to trex_allreduce_sum instead
+ *   trex_allreduce_sum: buf [count] fp32 device, in place, summed over ranks
+ * ---------------------------------------------------------------------- */
+int trex_comm_unique_id_bytes(void);
+int trex_comm_get_unique_id(void* id);
+int trex_comm_init(void** comm, int nranks, const void* id, int rank, int dev);
+int trex_comm_destroy(void* comm);
+int trex_allreduce_sum(float* buf, int count, int dev, void* comm, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -171,9 +171,12 @@ def test_c5_full_size_step_vs_fp64(device, gemm):
                                                                       cond)), err.max()
     del F, G64, S64, dS64
     # two more steps of the loop: parameters vs the oracle's optax adam.
-    # Adam's first updates are ~lr * sign(g), so a d tree_params entry within
-    # its conditioning bound of 0 (above) may take either sign in fp32: such
-    # entries (in any step) are exempt for tree_params, nothing else is.
+    # Adam's update is lr * m_hat / (sqrt(v_hat) + eps) with m_hat a running
+    # mean of the gradients: where a d tree_params entry, or m_hat itself (the
+    # steps' gradients cancelling), is within the gradient's conditioning
+    # bound of 0 (above), fp32 may move that parameter by up to ~2 lr in
+    # either direction.  Such entries are exempt for tree_params; nothing
+    # else is.
     ill = np.abs(ref_th) <= cond
     st = T.adam_init(p64)
     upd, st = T.adam_update(grads, st, lr=0.01)
@@ -183,15 +186,18 @@ def test_c5_full_size_step_vs_fp64(device, gemm):
         lk = float(opt.step(temps[k], nz, next_temperature=nxt))
         rl, gr = T.compute_loss(noise, p64, S, temps[k], None)
         np.testing.assert_allclose(lk, rl, rtol=SOFT_RTOL)
-        ill |= np.abs(gr["tree_params"]) <= cond
         upd, st = T.adam_update(gr, st, lr=0.01)
+        m_hat = st["mu"]["tree_params"] / (1 - 0.9 ** st["count"])
+        ill |= (np.abs(gr["tree_params"]) <= cond) | (np.abs(m_hat) <= 2 * cond)
         p64 = {kk: p64[kk] + upd[kk] for kk in p64}
     torch.cuda.synchronize()
     for k in p64:
         got = opt.params[k].cpu().numpy().astype(np.float64)
         bad = ~np.isclose(got, p64[k], rtol=5e-5, atol=5e-6)
         if k == "tree_params":
-            assert not (bad & ~ill).any(), int((bad & ~ill).sum())
+            hard = bad & ~ill
+            assert not hard.any(), (int(hard.sum()), float(np.abs(got - p64[k])[hard].max()),
+                                    float(np.abs(ref_th)[hard].min()), float(cond[hard].max()))
             assert ill.mean() < 1e-2
         else:
             assert not bad.any(), int(bad.sum())

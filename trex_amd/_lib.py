@@ -45,6 +45,12 @@ SIGNATURES = {
     "trex_sankoff_backtrack": (_c_i, [_p, _c_i, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
     "trex_dp_to_trex_layout": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p]),
     "trex_dp_site_major": (_c_i, [_c_i]),
+    # multi-GPU exchange (RCCL, dlopen'ed on first use)
+    "trex_comm_unique_id_bytes": (_c_i, []),
+    "trex_comm_get_unique_id": (_c_i, [_p]),
+    "trex_comm_init": (_c_i, [ctypes.POINTER(_p), _c_i, _p, _c_i, _c_i]),
+    "trex_comm_destroy": (_c_i, [_p]),
+    "trex_allreduce_sum": (_c_i, [_p, _c_i, _c_i, _p, _p]),
     # raw-table run_dp / backtrack_sankoff_jit
     "trex_run_dp": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _c_i, _p, _p, _p, _p]),
     "trex_backtrack_workspace_bytes": (_c_i64, [_c_i, _c_i]),

@@ -65,3 +65,51 @@ class GramReducer:
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(G, group=self.group)
         return G
+
+
+class NativeComm:
+    """The C ABI's RCCL exchange (trex_comm_* / trex_allreduce_sum in
+    include/trex_hip.h): what a binding without torch.distributed uses for
+    the sharded paths' one all-reduce.  ``unique_id`` comes from rank 0's
+    ``NativeComm.new_unique_id()`` and is shared out of band."""
+
+    def __init__(self, nranks: int, rank: int, unique_id: bytes, device_index: int):
+        import ctypes
+
+        from ._lib import check, lib
+
+        self.dev = int(device_index)
+        self.comm = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(unique_id), lib().trex_comm_unique_id_bytes())
+        check(lib().trex_comm_init(ctypes.byref(self.comm), int(nranks), buf, int(rank), self.dev))
+
+    @staticmethod
+    def new_unique_id() -> bytes:
+        import ctypes
+
+        from ._lib import check, lib
+
+        n = lib().trex_comm_unique_id_bytes()
+        buf = ctypes.create_string_buffer(n)
+        check(lib().trex_comm_get_unique_id(buf))
+        return buf.raw
+
+    def all_reduce_sum(self, t):
+        """In-place sum over ranks of a contiguous fp32 device tensor, on
+        torch's current stream."""
+        import torch
+
+        from ._lib import check, lib, stream_handle
+
+        if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("all_reduce_sum takes a contiguous fp32 device tensor")
+        check(lib().trex_allreduce_sum(t.data_ptr(), t.numel(), self.dev, self.comm,
+                                       stream_handle(t.device)))
+        return t
+
+    def close(self):
+        from ._lib import check, lib
+
+        if self.comm:
+            check(lib().trex_comm_destroy(self.comm))
+            self.comm = None

@@ -245,11 +245,20 @@ class Adam:
     """optax.adam(lr, b1, b2, eps) [chained after clip_by_global_norm(clip)].
 
     Updates the parameter tensors in place with one fused kernel per tensor.
+
+    ``sharded``: names of tensors whose gradient is split over the ranks of
+    ``group`` (site sharding: each rank holds a block of the tensor).  The
+    global norm of clip_by_global_norm then sums their squared-norm partials
+    over the ranks (one all-reduce of 512 fp64 partials per sharded tensor);
+    the other tensors are replicated and counted once.
     """
 
-    def __init__(self, params: dict, lr: float, b1=0.9, b2=0.999, eps=1e-8, clip_norm=None):
+    def __init__(self, params: dict, lr: float, b1=0.9, b2=0.999, eps=1e-8, clip_norm=None, *,
+                 sharded=(), group=None):
         torch = _torch()
         self.lr, self.b1, self.b2, self.eps, self.clip = lr, b1, b2, eps, clip_norm
+        self.sharded = frozenset(sharded)
+        self.group = group
         self.mu = {k: torch.zeros_like(v) for k, v in params.items()}
         self.nu = {k: torch.zeros_like(v) for k, v in params.items()}
         self.count = 0
@@ -265,6 +274,11 @@ class Adam:
             for i, k in enumerate(keys):
                 check(lib().trex_sq_norm_parts(ptr(grads[k]), grads[k].numel(),
                                                ptr(self.parts[512 * i:]), 512, st))
+                if k in self.sharded:
+                    import torch.distributed as dist
+
+                    if dist.is_available() and dist.is_initialized():
+                        dist.all_reduce(self.parts[512 * i:512 * (i + 1)], group=self.group)
             nparts = 512 * len(keys)
         for k in keys:
             p, g = params[k], grads[k]
@@ -289,7 +303,9 @@ class TreeOptimizer:
     (its leaf one-hot rows and ancestor logits for those sites).  The only
     exchange is an all-reduce of the N x N Gram matrix; every rank then
     computes the same loss, dA and tree_params update, and updates its own
-    ancestor logits.
+    ancestor logits.  With ``clip_norm`` (the evals path's
+    clip_by_global_norm(1.0), src/trex/evals/benchmark.py:70-71) one more
+    all-reduce sums the ancestors' squared-norm partials over the ranks.
 
     ``gemm``: "x3" (default) runs the two N x N x L*Q GEMMs as f16x3 split
     products on f16 MFMA (``trex_tree_gram_skip_x3`` / ``trex_tree_mf_rows_x3``;
@@ -317,8 +333,6 @@ class TreeOptimizer:
             from .distributed import GramReducer
 
             self.reducer = GramReducer(group)
-        if group is not None and clip_norm is not None:
-            raise NotImplementedError("clip_by_global_norm with site sharding")
         f32 = dict(dtype=torch.float32, device=dev)
         self.A = torch.empty((self.N, self.N), **f32)
         self.G = torch.empty((self.N, self.N), **f32)
@@ -329,7 +343,10 @@ class TreeOptimizer:
         self.grads = {k: torch.zeros_like(v) for k, v in self.params.items()}
         self.ws = torch.empty(int(lib().trex_tree_workspace_bytes(self.N, self.K)),
                               dtype=torch.uint8, device=dev)
-        self.opt = Adam(self.params, lr, clip_norm=clip_norm)
+        # with site sharding the ancestor logits are this rank's block of
+        # sites: clip_by_global_norm sums their squared norm over the ranks
+        self.opt = Adam(self.params, lr, clip_norm=clip_norm,
+                        sharded=("ancestors",) if group is not None else (), group=group)
         self._s_temperature = None  # temperature the S ancestor rows were computed with
         if gemm not in ("x3", "f32"):
             raise ValueError("gemm must be 'x3' or 'f32'")
