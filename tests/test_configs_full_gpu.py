@@ -12,12 +12,12 @@ size (VERDICT r01 "What's weak" 1):
       tau = 0.5): every tree score and the batch dC vs the OpenMP C
       restatement (fp64 accumulation) at rtol 1e-5, sampled trees vs the fp64
       oracle at rtol 1e-5, hard path (tau = 0) tree scores bit-exact;
-* C5  256 taxa (511 nodes) x 50 000 sites x 4 states, one full
-      TreeOptimizer.step for both GEMM precisions (f16x3 split products and
-      f32 MFMA): loss, Gram, dA, d loss / dS (ancestor rows) vs the fp64
-      oracle at rtol 1e-5 (atol 1e-5 * max|ref| for entries that cancel to
-      ~0), d tree_params at its fp32 conditioning bound (written in the
-      test), then two further steps' parameters vs the oracle loop.
+* C5  256 taxa (511 nodes) x 50 000 sites x 4 states, three
+      TreeOptimizer steps for both GEMM precisions (f16x3 split products and
+      f32 MFMA), each vs the fp64 oracle at the GPU's parameters before the
+      step: loss, Gram, dA, d loss / dS at rtol 1e-5, d tree_params at its
+      fp32 conditioning bound, the Adam updates of both parameter tensors
+      (see test_c5_full_size_steps_vs_fp64 for why per step).
       This is the only proof the x3 GEMMs hold at K = L*Q = 200 000.
 
 C3 at full size is in tests/test_sankoff_wide_gpu.py (test_c3_scale_properties).
@@ -132,72 +132,120 @@ def _close(got, ref, rtol=SOFT_RTOL):
     np.testing.assert_allclose(got, ref, rtol=rtol, atol=rtol * np.abs(ref).max())
 
 
+def _adam_tol(g, b, m0, v0, k, lr, b1=0.9, b2=0.999, eps=1e-8):
+    """Bound on |u(g') - u(g)| over |g' - g| <= b for one optax Adam update u
+    (scale_by_adam, bias-corrected, eps_root 0) from the same state (m0, v0):
+
+      |du/dg| <= lr [(1-b1)/(c1 (sqrt(v^) + eps)) + |m^| sqrt((1-b2)/c2) / (sqrt(v^) + eps)^2]
+
+    (using (1-b2)|g| / (c2 sqrt(v^)) <= sqrt((1-b2)/c2)), with |m^| maximised
+    and sqrt(v^) minimised over the interval; capped by 2 lr R_k, where
+    R_k = (1-b1)/c1 sqrt(c2/(1-b2)) sqrt(sum_i<k (b1^2/b2)^i) bounds |m^ / sqrt(v^)|
+    (Cauchy-Schwarz; R_1 = 1, R_3 ~ 1.004)."""
+    c1, c2 = 1.0 - b1 ** k, 1.0 - b2 ** k
+    ag = np.abs(g)
+    mh = (b1 * np.abs(m0) + (1 - b1) * (ag + b)) / c1
+    s = np.sqrt((b2 * v0 + (1 - b2) * np.maximum(ag - b, 0.0) ** 2) / c2)
+    D = (1 - b1) / (c1 * (s + eps)) + mh * np.sqrt((1 - b2) / c2) / (s + eps) ** 2
+    R = (1 - b1) / c1 * np.sqrt(c2 / (1 - b2)) * np.sqrt(sum((b1 * b1 / b2) ** i
+                                                            for i in range(k)))
+    return lr * np.minimum(b * D, 2 * R), 2 * lr * R
+
+
+def _adam64(p, g, m0, v0, k, lr, b1=0.9, b2=0.999, eps=1e-8):
+    m = b1 * m0 + (1 - b1) * g
+    v = b2 * v0 + (1 - b2) * g * g
+    return p - lr * (m / (1 - b1 ** k)) / (np.sqrt(v / (1 - b2 ** k)) + eps)
+
+
+def _f64(t):
+    return t.cpu().numpy().astype(np.float64)
+
+
 @pytest.mark.parametrize("gemm", ["x3", "f32"])
-def test_c5_full_size_step_vs_fp64(device, gemm):
+def test_c5_full_size_steps_vs_fp64(device, gemm):
+    """Three TreeOptimizer steps at C5 size (511 nodes x 50 000 sites x 4,
+    the bench's step), each checked against the fp64 oracle evaluated at the
+    GPU's own parameters before that step (tree.py:299-342 + optax adam):
+
+    * loss, Gram, dA and d loss / dS (ancestor rows) at rtol 1e-5 (atol
+      1e-5 * max|ref| for entries that cancel to ~0);
+    * d tree_params at its fp32 conditioning bound (written out below);
+    * tree_params after the step == the fp64 Adam update of the GPU's own
+      (exactly read back) gradient from the GPU's Adam state, to fp32 rounding;
+    * ancestor logits after the fused update_seq-VJP + Adam kernel == the fp64
+      Adam update of the fp64 gradient, within the propagation of the asserted
+      d loss / dS bound through update_seq's VJP and one Adam update
+      (_adam_tol); at most 1 % of entries may sit at the sign-flip cap.
+
+    A per-step check, not a comparison of two 3-step trajectories: Adam's
+    first update is lr * sign(g), so a gradient entry within its fp32 error
+    of 0 moves its parameter by +-lr either way, and two trajectories then
+    legitimately differ by O(lr) in those entries (seen at this size: a few
+    dozen of 130 050 tree_params).  This is the only proof the x3 GEMMs hold
+    at K = L*Q = 200 000."""
     from trex_amd import tree as G
 
     S, params, noise = _c5_case()
     n, L, Q = S.shape
     nl = (n + 1) // 2
+    lr = 0.01
     opt = G.TreeOptimizer(_dev(S, device), {k: _dev(v, device) for k, v in params.items()},
-                          lr=0.01, gemm=gemm)
+                          lr=lr, gemm=gemm)
     assert opt.gemm == gemm
     nz = _dev(noise, device)
     temps = [2.0, 1.9996, 1.9992]
-    loss = float(opt.step(temps[0], nz, next_temperature=temps[1]))
-    torch.cuda.synchronize()
-    # fp64 oracle of the same step (tree.py:299-342 at T = 2.0)
-    p64 = {k: v.astype(np.float64) for k, v in params.items()}
-    S64 = T.update_seq(p64["ancestors"], S, temps[0])
-    A64 = T.update_tree(p64["tree_params"], noise, 1.0)
-    F = S64.reshape(n, -1)
-    G64 = F @ F.T
-    _close(opt.G.cpu().numpy(), G64)
-    rloss, grads = T.compute_loss(noise, p64, S, temps[0], None)
-    np.testing.assert_allclose(loss, rloss, rtol=SOFT_RTOL)
-    _, dS64, dA64 = T.compute_surrogate_cost_grads(S64, A64)
-    dA64 = dA64 + temps[0] * T.enforce_graph_constraints_grad(A64, 10.0)
-    _close(opt.dA.cpu().numpy(), dA64)
-    _close(opt.dS[nl:].cpu().numpy(), dS64[nl:])
-    # d tree_params = A (dA - sum_k A dA) per row (softmax VJP, tree.py:50-107):
-    # dA ~ (E_i + E_j)/2 - G_ij ~ 5e4 here, so dA's own fp32 rounding (which
-    # the reference's fp32 autodiff has too) reaches d tree_params as
-    # ~eps32 * A_ij * max_k |dA_ik| -- the conditioning bound, written out:
-    g_th = opt.grads["tree_params"].cpu().numpy().astype(np.float64)
-    cond = 16 * 1.2e-7 * A64[:-1, nl:] * np.abs(dA64[:-1]).max(axis=1, keepdims=True)
-    ref_th = grads["tree_params"]
-    err = np.abs(g_th - ref_th)
-    assert np.all(err <= SOFT_RTOL * np.abs(ref_th).max() + np.maximum(SOFT_RTOL * np.abs(ref_th),
-                                                                      cond)), err.max()
-    del F, G64, S64, dS64
-    # two more steps of the loop: parameters vs the oracle's optax adam.
-    # Adam's update is lr * m_hat / (sqrt(v_hat) + eps) with m_hat a running
-    # mean of the gradients: where a d tree_params entry, or m_hat itself (the
-    # steps' gradients cancelling), is within the gradient's conditioning
-    # bound of 0 (above), fp32 may move that parameter by up to ~2 lr in
-    # either direction.  Such entries are exempt for tree_params; nothing
-    # else is.
-    ill = np.abs(ref_th) <= cond
-    st = T.adam_init(p64)
-    upd, st = T.adam_update(grads, st, lr=0.01)
-    p64 = {k: p64[k] + upd[k] for k in p64}
-    for k in (1, 2):
-        nxt = temps[k + 1] if k + 1 < len(temps) else temps[k]
-        lk = float(opt.step(temps[k], nz, next_temperature=nxt))
-        rl, gr = T.compute_loss(noise, p64, S, temps[k], None)
-        np.testing.assert_allclose(lk, rl, rtol=SOFT_RTOL)
-        upd, st = T.adam_update(gr, st, lr=0.01)
-        m_hat = st["mu"]["tree_params"] / (1 - 0.9 ** st["count"])
-        ill |= (np.abs(gr["tree_params"]) <= cond) | (np.abs(m_hat) <= 2 * cond)
-        p64 = {kk: p64[kk] + upd[kk] for kk in p64}
-    torch.cuda.synchronize()
-    for k in p64:
-        got = opt.params[k].cpu().numpy().astype(np.float64)
-        bad = ~np.isclose(got, p64[k], rtol=5e-5, atol=5e-6)
-        if k == "tree_params":
-            hard = bad & ~ill
-            assert not hard.any(), (int(hard.sum()), float(np.abs(got - p64[k])[hard].max()),
-                                    float(np.abs(ref_th)[hard].min()), float(cond[hard].max()))
-            assert ill.mean() < 1e-2
-        else:
-            assert not bad.any(), int(bad.sum())
+    losses = []
+    for k in range(3):
+        T_k = temps[k]
+        nxt = temps[k + 1] if k + 1 < len(temps) else T_k
+        p64 = {kk: _f64(v) for kk, v in opt.params.items()}
+        mu0 = {kk: _f64(v) for kk, v in opt.opt.mu.items()}
+        nu0 = {kk: _f64(v) for kk, v in opt.opt.nu.items()}
+        loss = float(opt.step(T_k, nz, next_temperature=nxt))
+        torch.cuda.synchronize()
+        losses.append(loss)
+        # fp64 oracle at the GPU's parameters before this step
+        S64 = T.update_seq(p64["ancestors"], S, T_k)
+        A64 = T.update_tree(p64["tree_params"], noise, 1.0)
+        val, dS64, dA64 = T.compute_surrogate_cost_grads(S64, A64)
+        dA64 = dA64 + T_k * T.enforce_graph_constraints_grad(A64, 10.0)
+        rloss = val + T_k * T.enforce_graph_constraints(A64, 10.0)
+        np.testing.assert_allclose(loss, rloss, rtol=SOFT_RTOL)
+        F = S64.reshape(n, -1)
+        _close(opt.G.cpu().numpy(), F @ F.T)
+        del F
+        _close(opt.dA.cpu().numpy(), dA64)
+        _close(opt.dS[nl:].cpu().numpy(), dS64[nl:])
+        # d tree_params = A (dA - sum_k A dA) per row (softmax VJP, tree.py:50-107):
+        # dA ~ (E_i + E_j)/2 - G_ij ~ 5e4 here, so dA's own fp32 rounding (which
+        # the reference's fp32 autodiff has too) reaches d tree_params as
+        # ~eps32 * A_ij * max_k |dA_ik| -- the conditioning bound, written out:
+        g_th = _f64(opt.grads["tree_params"])
+        ref_th = T.update_tree_vjp(p64["tree_params"], noise, 1.0, None, A64, dA64)
+        cond = 16 * 1.2e-7 * A64[:-1, nl:] * np.abs(dA64[:-1]).max(axis=1, keepdims=True)
+        err = np.abs(g_th - ref_th)
+        assert np.all(err <= SOFT_RTOL * np.abs(ref_th).max()
+                      + np.maximum(SOFT_RTOL * np.abs(ref_th), cond)), err.max()
+        # tree_params: fp64 Adam of the GPU's own gradient, to fp32 rounding
+        new_th = _f64(opt.params["tree_params"])
+        want = _adam64(p64["tree_params"], g_th, mu0["tree_params"], nu0["tree_params"],
+                       k + 1, lr)
+        slack = 4.8e-7 * np.abs(want) + 1e-5 * lr
+        assert np.all(np.abs(new_th - want) <= slack), np.abs(new_th - want).max()
+        # ancestors: fused VJP + Adam vs fp64, error propagated from dS's bar
+        anc = p64["ancestors"]
+        S_anc = S64[nl:]
+        g_anc = T.update_seq_vjp(anc, T_k, S_anc, dS64[nl:])
+        e_dS = SOFT_RTOL * np.abs(dS64[nl:]).max()
+        # |d g| <= T S (|d dS| + sum_q S |d dS|) + fp32 rounding of the VJP
+        b = T_k * S_anc * (2 * e_dS + 8 * 1.2e-7 * np.abs(dS64[nl:]).max(axis=-1, keepdims=True))
+        del S64, dS64
+        tol, cap = _adam_tol(g_anc, b, mu0["ancestors"], nu0["ancestors"], k + 1, lr)
+        want = _adam64(anc, g_anc, mu0["ancestors"], nu0["ancestors"], k + 1, lr)
+        new_anc = _f64(opt.params["ancestors"])
+        err = np.abs(new_anc - want)
+        assert np.all(err <= tol + 4.8e-7 * np.abs(want) + 1e-5 * lr), (err - tol).max()
+        assert np.mean(tol >= cap) < 1e-2
+        del anc, S_anc, g_anc, b, tol, want, new_anc, err
+    assert losses[0] > losses[1] > losses[2]
