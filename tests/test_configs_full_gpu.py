@@ -48,15 +48,19 @@ def _dev(x, device, dtype=None):
     return t.to(device).contiguous()
 
 
-@pytest.mark.parametrize("kernel", ["0", "1", "auto"])
+@pytest.mark.parametrize("kernel", ["0", "1", "staged", "auto"])
 def test_c2_full_size_hard_dp_table_bitexact(device, kernel, monkeypatch):
     """C2 at full size, tau = 0: trex's (L, n_all, Q) DP table, the total and
     the reconstruction equal the fp32 restatement bit for bit.  kernel "0" =
-    lane-per-site, "1" = state-parallel (G = 4, DPP quads), "auto" = policy."""
+    lane-per-site, "1" = state-parallel (G = 4, DPP quads), "staged" = the
+    state-parallel items as workgroups over the tree's levels, "auto" =
+    policy."""
     if kernel == "auto":
         monkeypatch.delenv("TREX_WIDE_SMALLQ", raising=False)
+        monkeypatch.delenv("TREX_STAGED", raising=False)
     else:
-        monkeypatch.setenv("TREX_WIDE_SMALLQ", kernel)
+        monkeypatch.setenv("TREX_WIDE_SMALLQ", "1" if kernel == "staged" else kernel)
+        monkeypatch.setenv("TREX_STAGED", "1" if kernel == "staged" else "0")
     nl, L, Q = 64, 10000, 4
     seqs, adj = simulate_leaves(nl, L, Q, 5, seed=1)
     cost = hamming(Q)

@@ -106,6 +106,96 @@ def test_plan_program_reproduces_oracle(kind):
     assert plan.backtrack_ok == (0 if kind == "cycle" else 1)
 
 
+STAGE_WAVES = 8  # kStageWaves (trex_common.h)
+
+
+def _staged(plan, b):
+    """Decode tree b's staged region (trex_common.h): steps, S, offsets."""
+    from trex_amd._lib import TREX_PLAN_HEADER_INTS
+
+    ni, W = plan.n_int, STAGE_WAVES
+    stride = 4 * ni + ((ni * W + 2 + 3) & ~3)
+    base = TREX_PLAN_HEADER_INTS + plan.B * ni * 6 + b * stride
+    r = plan.host[base:base + stride]
+    S = int(r[4 * ni])
+    return r[:4 * ni].reshape(ni, 4), S, r[4 * ni + 1:4 * ni + 2 + S * W]
+
+
+@pytest.mark.parametrize("kind", ["random", "balanced", "fwdref", "dag", "cycle"])
+def test_staged_program_reproduces_oracle(kind):
+    """The staged (multi-wave) program of sankoff_staged.hip: run with the
+    waves of every stage in reverse order (any interleaving must do), it
+    reproduces the oracle DP table; in the adjoint order no two waves of a
+    stage write one cotangent slot, every slot is set before it is
+    accumulated into or read, and the DAG quirk runs serially on wave 0."""
+    if kind == "random":
+        ch = random_topologies(4, 40, seed=1)
+    elif kind == "balanced":
+        ch = balanced_children(64, B=2)
+    else:
+        ch = weird_children(kind)[None]
+    plan = TreePlan(ch)
+    n_all = ch.shape[1]
+    nl = (n_all + 1) // 2
+    ni = n_all - nl
+    W = STAGE_WAVES
+    leaves = random_leaves(ch.shape[0], nl, 11, 4, seed=2, missing=0.1)
+    cost = int_cost(4, seed=3).astype(np.float64)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, 0.0)
+    for b in range(ch.shape[0]):
+        steps, S, offs = _staged(plan, b)
+        assert np.all(np.diff(offs) >= 0) and offs[0] == 0 and offs[-1] == ni
+        assert sorted(steps[:, 0] & 0xFFFF) == list(range(ni))
+        stage_of = {}
+        for s in range(S):
+            for w in range(W):
+                for k in range(offs[s * W + w], offs[s * W + w + 1]):
+                    stage_of[int(steps[k, 0] & 0xFFFF)] = (s, w, k)
+        if plan.n_dag_nodes:
+            assert S == 1 and all(v[1] == 0 for v in stage_of.values())
+        lD = leaf_dp(leaves[b], 4)
+        dp = np.full((ni, 11, 4), np.nan)
+        for s in range(S):
+            for w in reversed(range(W)):
+                for k in range(offs[s * W + w], offs[s * W + w + 1]):
+                    row, da, db, flags = (int(x) for x in steps[k])
+                    acc = np.zeros((11, 4))
+                    for d in (da, db):
+                        kind_ = (d >> 24) & 3
+                        if kind_ == 1:
+                            D = lD[d & 0xFFFF]
+                        elif kind_ == 2:
+                            D = dp[d & 0xFFFF]
+                            assert not np.isnan(D).any(), "child not computed in an earlier stage"
+                            cs = stage_of[d & 0xFFFF]
+                            assert cs[0] < s or (cs[1] == w and cs[2] < k)
+                        else:
+                            D = np.full((11, 4), SENTINEL)
+                        acc = acc + (cost[None] + D[:, None, :]).min(axis=2)
+                    dp[row & 0xFFFF] = acc
+        np.testing.assert_array_equal(dp.transpose(0, 2, 1), ref["dp"][b])
+        # adjoint: stages and each wave's steps reversed
+        state = {ni - 1: "set"}
+        for s in reversed(range(S)):
+            writers = {}
+            for w in range(W):
+                for k in reversed(range(offs[s * W + w], offs[s * W + w + 1])):
+                    row, da, db, flags = (int(x) for x in steps[k])
+                    if flags & 2:  # unreached
+                        continue
+                    assert state.get(row & 0xFFFF) == "set", "cotangent read before it is set"
+                    for d in (da, db):
+                        if (d >> 24) & 3 != 2:
+                            continue
+                        c = d & 0xFFFF
+                        assert writers.setdefault(c, w) == w, "two waves write one slot in a stage"
+                        if d & (1 << 26):
+                            assert state.get(c) == "set", "accumulate into an unset slot"
+                        else:
+                            assert c not in state, "slot set twice"
+                        state[c] = "set"
+
+
 def test_plan_slot_counts_are_sethi_ullman():
     """Sethi-Ullman depth minus the register bypass: the child evaluated
     right before its parent never takes a slot, so a balanced tree of n

@@ -26,19 +26,25 @@ pytestmark = pytest.mark.gpu
 SOFT_RTOL = 1e-5
 
 
-@pytest.fixture(autouse=True, params=["lane-per-site", "state-parallel", "auto"])
+@pytest.fixture(autouse=True, params=["lane-per-site", "state-parallel", "staged", "auto"])
 def q4_kernel(request, monkeypatch):
-    """Every Q <= 4 case runs three times: on the lane-per-site kernel (the
+    """Every Q <= 4 case runs four times: on the lane-per-site kernel (the
     C4 headline path), on the state-parallel kernel (4 lanes per site, one
-    DPP quad, G = 4; Q = 2 / 3 pad the quad), and under the library's policy
-    (sankoff.hip wide_small_q: grids of at most ~1.5 64-site waves per CU go
-    state-parallel)."""
+    DPP quad, G = 4; Q = 2 / 3 pad the quad), on the staged kernel (the
+    state-parallel item as a workgroup of waves over the tree's levels,
+    sankoff_staged.hip) and under the library's policy (sankoff.hip
+    wide_small_q / use_staged: small grids go staged)."""
     if request.param == "lane-per-site":
         monkeypatch.setenv("TREX_WIDE_SMALLQ", "0")
     elif request.param == "state-parallel":
         monkeypatch.setenv("TREX_WIDE_SMALLQ", "1")
+        monkeypatch.setenv("TREX_STAGED", "0")
+    elif request.param == "staged":
+        monkeypatch.setenv("TREX_WIDE_SMALLQ", "1")
+        monkeypatch.setenv("TREX_STAGED", "1")
     else:
         monkeypatch.delenv("TREX_WIDE_SMALLQ", raising=False)
+        monkeypatch.delenv("TREX_STAGED", raising=False)
     return request.param
 
 

@@ -25,6 +25,14 @@ pytestmark = pytest.mark.gpu
 SOFT_RTOL = 1e-5
 
 
+@pytest.fixture(autouse=True, params=["wave", "staged"])
+def wide_kernel(request, monkeypatch):
+    """Every case runs on the one-wave-per-item kernel (sankoff_wide.hip)
+    and on the staged workgroup kernel (sankoff_staged.hip)."""
+    monkeypatch.setenv("TREX_STAGED", "1" if request.param == "staged" else "0")
+    return request.param
+
+
 def _engine(children, L, Q, device):
     return SankoffEngine(TreePlan(children), L, Q, device)
 

@@ -254,6 +254,85 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
   return true;
 }
 
+// Staged program of one tree (layout: trex_common.h).  Nodes are levelled by
+// height over real internal edges (a leaf / 1e5-row child adds nothing), each
+// level is one stage, its nodes dealt round-robin to the workgroup's waves:
+// a stage's nodes depend only on earlier stages, so the waves run them in
+// parallel and the serial chain is the tree height (6 for a balanced
+// 64-taxon tree instead of 63 nodes).  A topology with a shared internal
+// child (trex's DAG quirk) runs serially on wave 0 in index order, where the
+// accumulate flags order its cotangent sums exactly as the single-wave
+// kernels do.
+void stage_one_tree(const int32_t* ch, int n_all, int32_t* region) {
+  const int nl = (n_all + 1) / 2;
+  const int ni = n_all - nl;
+  constexpr int W = kStageWaves;
+  std::vector<int> kind(2 * ni), idx(2 * ni), refs(ni, 0), height(ni, 1);
+  for (int r = 0; r < ni; ++r) {
+    const int node = nl + r;
+    for (int k = 0; k < 2; ++k) {
+      const int c = ch[2 * node + k];  // validated by plan_one_tree
+      if (c == -1 || c >= node) {
+        kind[2 * r + k] = kKindSent;
+        idx[2 * r + k] = 0;
+      } else if (c < nl) {
+        kind[2 * r + k] = kKindLeaf;
+        idx[2 * r + k] = c;
+      } else {
+        kind[2 * r + k] = kKindInt;
+        idx[2 * r + k] = c - nl;
+        refs[c - nl] += 1;
+        height[r] = std::max(height[r], height[c - nl] + 1);
+      }
+    }
+  }
+  const bool dag = std::any_of(refs.begin(), refs.end(), [](int v) { return v > 1; });
+  std::vector<char> reach(ni, 0);
+  reach[ni - 1] = 1;
+  for (int r = ni - 1; r >= 0; --r)
+    if (reach[r])
+      for (int k = 0; k < 2; ++k)
+        if (kind[2 * r + k] == kKindInt) reach[idx[2 * r + k]] = 1;
+  // (stage, wave) of every row
+  int S = 1;
+  std::vector<int> stage(ni, 0), wave(ni, 0);
+  if (!dag) {
+    S = *std::max_element(height.begin(), height.end());
+    std::vector<int> fill(S, 0);
+    for (int r = 0; r < ni; ++r) {
+      stage[r] = height[r] - 1;
+      wave[r] = fill[stage[r]]++ % W;
+    }
+  }
+  std::vector<int> order(ni);
+  for (int r = 0; r < ni; ++r) order[r] = r;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+    return stage[x] != stage[y] ? stage[x] < stage[y] : wave[x] < wave[y];
+  });
+  int32_t* steps = region;
+  int32_t* offs = region + 4LL * ni + 1;
+  region[4LL * ni] = S;
+  for (int j = 0; j <= S * W; ++j) offs[j] = ni;
+  for (int k = ni - 1; k >= 0; --k) offs[stage[order[k]] * W + wave[order[k]]] = k;
+  for (int j = S * W - 1; j >= 0; --j) offs[j] = std::min(offs[j], offs[j + 1]);
+  // accumulate flags follow the adjoint's order: stages, then steps, reversed
+  std::vector<char> seen(ni, 0);
+  for (int k = ni - 1; k >= 0; --k) {
+    const int r = order[k];
+    int32_t* e = steps + 4LL * k;
+    e[0] = r & 0xFFFF;
+    for (int j = 0; j < 2; ++j) {
+      int32_t d = (idx[2 * r + j] & 0xFFFF) | (kind[2 * r + j] << 24);
+      if (kind[2 * r + j] == kKindInt && reach[r]) {
+        if (seen[idx[2 * r + j]]) d |= kStepAccumulate;
+        seen[idx[2 * r + j]] = 1;
+      }
+      e[1 + j] = d;
+    }
+    e[3] = (r == ni - 1 ? kStepRoot : 0) | (reach[r] ? 0 : kStepUnreached);
+  }
+}
+
 }  // namespace
 
 }  // namespace trex
@@ -261,7 +340,7 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
 extern "C" int64_t trex_plan_ints(int B, int n_all) {
   if (B <= 0 || n_all < 2) return 0;
   const int ni = n_all - (n_all + 1) / 2;
-  return TREX_PLAN_HEADER_INTS + (int64_t)B * ni * 6;
+  return TREX_PLAN_HEADER_INTS + (int64_t)B * ni * 6 + (int64_t)B * trex::staged_tree_ints(ni);
 }
 
 extern "C" int trex_plan_build(const int32_t* children, int B, int n_all,
@@ -274,12 +353,14 @@ extern "C" int trex_plan_build(const int32_t* children, int B, int n_all,
   std::memset(plan, 0, sizeof(int32_t) * TREX_PLAN_HEADER_INTS);
   int32_t* fwd = plan + TREX_PLAN_HEADER_INTS;
   int32_t* bt = fwd + (int64_t)B * ni * 4;
+  int32_t* staged = bt + (int64_t)B * ni * 2;
   int max_slots = 0, all_bt_ok = 1, dag = 0, unr = 0;
   for (int b = 0; b < B; ++b) {
     int s = 0, ok = 0, d = 0, u = 0;
     if (!plan_one_tree(children + (int64_t)b * n_all * 2, n_all, fwd + (int64_t)b * ni * 4,
                        bt + (int64_t)b * ni * 2, &s, &ok, &d, &u))
       return set_error(TREX_E_TOPOLOGY, "trex_plan_build: tree %d has an invalid child list", b);
+    stage_one_tree(children + (int64_t)b * n_all * 2, n_all, staged + b * staged_tree_ints(ni));
     max_slots = std::max(max_slots, s);
     all_bt_ok &= ok;
     dag += d;

@@ -1292,6 +1292,18 @@ bool wide_small_q(int B, int L, int Q) {
   return (int64_t)B * ((L + kWave - 1) / kWave) * 2 <= (int64_t)3 * device_cus();
 }
 
+// Grids of at most about one state-parallel wave per SIMD (C2: one tree x
+// 625 16-site items) run the staged kernel (sankoff_staged.hip): one
+// workgroup of waves per item, the tree's levels spread over the waves, so
+// the serial chain is the tree height instead of every internal node.
+// TREX_STAGED=0 / 1 forces it off / on (whenever its LDS fits; A/B, tests).
+bool use_staged(int B, int L, int Q, int ni, int nl, int phase) {
+  if (staged_lds_bytes(ni, nl, Q, phase) > kLdsPerCu) return false;
+  const char* e = std::getenv("TREX_STAGED");  // read per call (tests flip it)
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  return (int64_t)B * wide_tiles(L, Q) <= (int64_t)4 * device_cus();
+}
+
 int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const int8_t* leaves,
               const float* cost, int B, int L, int n_all, int Q, float tau, unsigned flags,
               float* dp, float* site_score, float* tree_score, const float* dts, float* d_cost,
@@ -1349,6 +1361,8 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
     c.d_cost = d_cost;
     c.workspace = workspace;
     c.stream = stream;
+    if (use_staged(B, L, Q, s.ni, s.nl, phase))
+      return staged_run(fn, c, plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 6);
     return wide_run(fn, c);
   }
   if ((int64_t)s.ni * L * Q * 4 > 0x7FFFFFF0LL)

@@ -24,6 +24,18 @@ constexpr int32_t kStepRoot = 1;
 constexpr int32_t kStepUnreached = 2;
 constexpr int32_t kStepToNext = 4;  // output consumed only by the next step (bypass)
 
+// Staged (multi-wave) program, after the backtrack entries of a plan: one
+// region of staged_tree_ints(ni) ints per tree, steps [ni][4] (same words as
+// the forward steps; every internal row has its own LDS slot = its row, so
+// no slot / bypass fields) | S (stages) | offsets [S * kStageWaves + 1]:
+// steps of stage s on wave w are [off[s*W + w], off[s*W + w + 1]).  The
+// waves of one workgroup run a stage's node lists in parallel, a barrier
+// between stages (sankoff_staged.hip).
+constexpr int kStageWaves = 8;
+inline int64_t staged_tree_ints(int ni) {
+  return 4LL * ni + (((int64_t)ni * kStageWaves + 2 + 3) & ~3LL);
+}
+
 // backtrack entry kinds (bits 16-19 of word 0)
 constexpr int kBtRoot = 0;
 constexpr int kBtReal = 1;
@@ -78,6 +90,10 @@ int wide_tiles(int L, int Q);
 size_t wide_lds_bytes(int n_slots, int nl, int Q);
 int64_t wide_workspace_bytes(int B, int L, int Q);
 int wide_run(const char* fn, const WideCall& c);
+// staged multi-wave kernel (sankoff_staged.hip); staged = the plan's staged
+// regions (after the backtrack entries)
+size_t staged_lds_bytes(int ni, int nl, int Q, int phase);
+int staged_run(const char* fn, const WideCall& c, const int32_t* staged);
 // fixed-order sum of per-item partials -> tree_score [B] (phase & 1), d_cost
 // [Q*Q] (phase & 2); part_dc is [Q*Q][B*tiles]
 // (ragged batches: first[b * first_stride] is tree b's first item, items the
