@@ -34,7 +34,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--trees-per-gpu", type=int, default=128)
+    ap.add_argument("--trees", type=int, default=1024,
+                    help="C4 batch size, split over the ranks (strong scaling)")
     ap.add_argument("--taxa", type=int, default=32)
     ap.add_argument("--sites", type=int, default=5000)
     ap.add_argument("--states", type=int, default=4)
@@ -46,22 +47,58 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 tree-cost loop line")
     ap.add_argument("--no-nk", action="store_true", help="skip the NK landscape-aware line")
     ap.add_argument("--no-ragged", action="store_true", help="skip the ragged-batch line")
+    ap.add_argument("--no-shard", action="store_true", help="skip the 128-tree shard line")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def make_inputs(torch, device, B, n, L, Q, rank):
+def make_inputs(torch, device, n_trees, n, L, Q, lo, hi):
+    """Trees [lo, hi) of the C4 batch (random coalescent
+    topologies, seed 4; iid uniform leaf states, seed 5): the same global
+    batch for every rank count, so N ranks split exactly C4's work."""
     from trex_amd import TreePlan, random_topologies
 
-    ch = random_topologies(B, n, seed=4 + 1000 * rank)
+    ch = random_topologies(n_trees, n, seed=4)[lo:hi]
     plan = TreePlan(ch)
     g = torch.Generator(device=device)
-    g.manual_seed(5 + 1000 * rank)
-    leaves = torch.randint(0, Q, (B, n, L), generator=g, device=device, dtype=torch.int8)
+    g.manual_seed(5)
+    leaves = torch.randint(0, Q, (n_trees, n, L), generator=g, device=device,
+                           dtype=torch.int8)[lo:hi].contiguous()
     cost = (torch.ones(Q, Q) - torch.eye(Q)).to(device=device, dtype=torch.float32)
     return ch, plan, leaves, cost
+
+
+def host_cpu():
+    """The host's CPU model and the cores this job may use: the affinity
+    mask, capped by a cgroup CPU quota and by OMP_NUM_THREADS when the
+    environment sets it (the GPU box's per-GPU CPU share)."""
+    info = {"model": None, "cpus_online": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                info["cgroup_quota_cpus"] = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    use = info["affinity_cpus"]
+    if info["cgroup_quota_cpus"]:
+        use = min(use, max(1, int(info["cgroup_quota_cpus"])))
+    if info["omp_num_threads"] and info["omp_num_threads"].isdigit():
+        use = min(use, int(info["omp_num_threads"]))
+    info["threads_used"] = use
+    return info, use
 
 
 class Step:
@@ -110,6 +147,23 @@ def time_kernels(torch, step, iters=20):
     return out
 
 
+def shard_line(torch, device, ch, leaves, cost, tau, L, Q, n, Bs):
+    """The slice of C4 each rank runs at N = 8 (128 trees), alone on one GPU:
+    fused fwd + grad (hipGraph replay) and the fused kernel's event time."""
+    from trex_amd import SankoffEngine, TreePlan
+
+    eng = SankoffEngine(TreePlan(ch[:Bs]), L, Q, device)
+    st = Step(torch, eng, leaves[:Bs].contiguous(), cost, tau)
+    sec = _replay_seconds(torch, st, 200)
+    kt = time_kernels(torch, st)["sankoff_fwd_bwd"]
+    fb = Bs * L * (2 * n + 8 * Q * (n - 1))
+    return {"workload": f"C4 / 8: {Bs} trees x {L} sites x {n} taxa x {Q} states, softmin "
+                        f"tau={tau} fwd + grad (one rank's share at N = 8), hipGraph replay",
+            "ms_per_step": sec * 1e3, "value": Bs * L * (n - 1) * Q / sec,
+            "fused_kernel_us": round(kt * 1e6, 2), "algorithmic_bytes": fb,
+            "hbm_frac": round(fb / kt / 1e9 / HBM_PEAK_GBS, 4)}
+
+
 def c2_line(torch, device, args, cpu_threads):
     """C2 (BASELINE.json configs[1]): one balanced 64-taxa tree x 10k sites x
     4 states, softmin fwd+grad (tau 1.0), leaves simulated along the tree."""
@@ -153,7 +207,20 @@ def c2_line(torch, device, args, cpu_threads):
         reps.append(time.perf_counter() - t0)
     cpu_s = float(np.median(reps))
     out["cpu_port_ms"] = cpu_s * 1e3
+    out["cpu_port_threads"] = cpu_threads
     out["speedup_vs_cpu_port"] = cpu_s / gpu_s
+    # trex-structure numpy proxy at the full C2 size: run_sankoff's layout
+    # (dp + bt tables, vectorised over sites, serial over nodes), hard
+    # forward only (trex's run_sankoff has no gradient of its own)
+    from oracle.sankoff_ref import run_sankoff_ref
+
+    t0 = time.perf_counter()
+    run_sankoff_ref(adj, (np.ones((4, 4)) - np.eye(4)).astype(np.float32),
+                    seqs[:64].astype(np.float32), 127, 4, 64)
+    px = time.perf_counter() - t0
+    out["trex_numpy_proxy"] = {"ms": px * 1e3, "value": units / px, "cores": 1,
+                               "sample": "full C2 (1 tree x 10000 sites x 64 taxa), hard "
+                                         "forward only, oracle/sankoff_ref.run_sankoff_ref"}
     return out
 
 
@@ -245,7 +312,66 @@ def c3_line(torch, device, cpu_threads):
     return res
 
 
-def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
+MFMA_F16_DENSE_TFS = 2500.0  # MI355X dense f16/bf16 MFMA peak (MI355X_MICROARCH.md)
+MFMA_F32_TFS = 157.0         # MI355X f32 matrix peak
+
+
+def c5_gemm_kernels(torch, opt):
+    """HIP-event time of the step's two GEMM launches on the optimiser's own
+    buffers, with their algorithmic HBM bytes and (f16x3) the MFMA flops the
+    tile plan issues -- executed work, not a trex-equivalent rate."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    L_ = lib()
+    st = stream_handle(opt.S.device)
+    cs = torch.cuda.current_stream(opt.S.device)
+    N, K, nl, na = opt.N, opt.K, opt.n_leaf, opt.n_anc
+    dS = opt.dS[nl:]
+    if opt.gemm == "x3":
+        gram = lambda: check(L_.trex_tree_gram_skip_x3(ptr(opt.S), N, K, opt.skip_rows, 1.0,  # noqa: E731
+                                                       ptr(opt.G), ptr(opt.ws), opt.ws.numel(), st))
+        mf = lambda: check(L_.trex_tree_mf_rows_x3(ptr(opt.M), ptr(opt.S), N, K, nl, na,  # noqa: E731
+                                                   float(N + 1), 1.0, ptr(dS), st))
+    else:
+        gram = lambda: check(L_.trex_tree_gram_skip(ptr(opt.S), N, K, opt.skip_rows, ptr(opt.G),  # noqa: E731
+                                                    ptr(opt.ws), opt.ws.numel(), st))
+        mf = lambda: check(L_.trex_tree_mf_rows(ptr(opt.M), ptr(opt.S), N, K, nl, na, ptr(dS),  # noqa: E731
+                                                st))
+
+    def timed(fn, reps=20):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cs)
+        for _ in range(reps):
+            fn()
+        e1.record(cs)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    out = {}
+    nt, sk = (N + 31) // 32, opt.skip_rows // 32
+    tiles = nt * (nt + 1) // 2 - sk * (sk + 1) // 2
+    for name, fn, abytes, flops in (
+            ("gram", gram, N * K * 4 + N * N * 4, tiles * 32 * 32 * K * 2),
+            ("mf", mf, N * K * 4 + N * N * 4 + na * K * 4, ((na + 31) // 32 * 32) * nt * 32 * K * 2)):
+        sec = timed(fn)
+        d = {"us": round(sec * 1e6, 2), "algorithmic_bytes": abytes,
+             "GBs": round(abytes / sec / 1e9, 1), "hbm_frac": round(abytes / sec / 1e9 / HBM_PEAK_GBS, 4)}
+        if opt.gemm == "x3":
+            issued = 3 * flops  # hi*hi + hi*lo + lo*hi on f16 MFMA
+            d.update(mfma_flops_issued=issued,
+                     mfma_tflops=round(issued / sec / 1e12, 1),
+                     mfma_frac=round(issued / sec / 1e12 / MFMA_F16_DENSE_TFS, 4),
+                     mfma_peak_tflops=MFMA_F16_DENSE_TFS)
+        else:
+            d.update(mfma_flops_issued=flops, mfma_tflops=round(flops / sec / 1e12, 1),
+                     mfma_frac=round(flops / sec / 1e12 / MFMA_F32_TFS, 4),
+                     mfma_peak_tflops=MFMA_F32_TFS)
+        out[name] = d
+    return out
+
+
+def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3"):
     """C5 (BASELINE.json configs[4]): 256 taxa (511 nodes) x 50 000 sites x 4
     states, joint Adam optimisation step (update_seq, update_tree, surrogate
     + graph constraint, their VJPs, optax Adam) -- trex's
@@ -275,7 +401,7 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
         import torch.distributed as dist
 
         group = dist.group.WORLD
-    opt = TreeOptimizer(S, params, lr=0.01, group=group)
+    opt = TreeOptimizer(S, params, lr=0.01, group=group, gemm=gemm)
     def temp(k):  # the annealing schedule of tests/test_convergence.py:260
         return max(0.1, 2.0 * (1.0 - k / 5000))
 
@@ -293,20 +419,28 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1):
         t = torch.tensor([sec], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         sec = float(t.item())
-    # trex's GEMM work per step: G = S S^T and dS = M S, both N x N x L*Q.  The
-    # build executes less (symmetric Gram tiles; dS for ancestor rows only),
-    # so this is a trex-equivalent rate, not the MFMA utilisation.
-    flops = 4.0 * n * n * L * Q
-    gemm_desc = ("f16x3 split-product MFMA GEMMs (f32 accumulate; held to rtol 1e-5 vs fp64 "
-                 "like the f32 path)" if opt.gemm == "x3" else "f32 MFMA GEMMs")
-    return {"workload": "C5: 511-node relaxed tree x 50000 sites x 4 states, joint Adam step "
-                        "(surrogate + constraint + VJPs + optax adam), " + gemm_desc
-                        + (f"; sites sharded over {world} ranks, Gram all-reduce" if world > 1
-                           else ""),
-            "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec, "n_gpus": world,
-            "scaling": "strong" if world > 1 else None,
-            "trex_equivalent_gemm_tflops": flops / sec / 1e12, "loss_last": float(loss),
-            "gemm": opt.gemm}
+    # algorithmic HBM bytes of one step (the step is HBM-bound overall): the
+    # Gram reads S once, the MF reads S and writes the ancestor rows of dS,
+    # the fused update_seq-VJP + Adam pass reads dS and the ancestors' logits
+    # / moments, writes logits / moments and the next step's S rows
+    Kl = (hi - lo) * Q
+    na = nl - 1
+    step_bytes = n * Kl * 4 + (n * Kl * 4 + na * Kl * 4) + na * Kl * 4 * 8
+    gemm_desc = ("f16x3 split-product MFMA GEMMs (f32 accumulate; rtol 1e-5 vs fp64 at this "
+                 "size, tests/test_configs_full_gpu.py)" if opt.gemm == "x3" else "f32 MFMA GEMMs")
+    res = {"workload": "C5: 511-node relaxed tree x 50000 sites x 4 states, joint Adam step "
+                       "(surrogate + constraint + VJPs + optax adam), " + gemm_desc
+                       + (f"; sites sharded over {world} ranks, Gram all-reduce" if world > 1
+                          else ""),
+           "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec, "n_gpus": world,
+           "scaling": "strong" if world > 1 else None, "loss_last": float(loss),
+           "gemm": opt.gemm,
+           "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": step_bytes,
+                        "achieved": round(step_bytes / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(step_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}}
+    if world == 1:
+        res["kernels"] = c5_gemm_kernels(torch, opt)
+    return res
 
 
 def ragged_line(torch, device, steps=20, warmup=3):
@@ -405,18 +539,6 @@ def cpu_baseline(ch, leaves_np, cost_np, tau, L, n, Q, threads):
             "kind": "port",
             "sample": f"{nb} trees x {L} sites x {n} taxa x {Q} states softmin fwd+grad "
                       f"(oracle/cpu_port.c, OpenMP, median of {len(reps)})"}
-    # trex-structure numpy proxy (sankoff.py layout: dp + bt tables, hard fwd)
-    from oracle.sankoff_ref import run_sankoff_ref
-    from trex_amd.topology import adjacency_from_children
-
-    adj = adjacency_from_children(ch[:1])[0]
-    seqs = leaves_np[0].astype(np.float32)
-    t0 = time.perf_counter()
-    run_sankoff_ref(adj, cost_np, seqs, 2 * n - 1, Q, n)
-    px = time.perf_counter() - t0
-    base["trex_numpy_proxy"] = {"value": L * (n - 1) * Q / px, "unit": "site-node-state updates/s",
-                                "cores": 1, "sample": f"1 tree x {L} sites hard forward only "
-                                "(oracle/sankoff_ref.run_sankoff_ref, dp+bt tables as trex)"}
     return base
 
 
@@ -443,9 +565,12 @@ def main():
             dist.init_process_group("nccl", device_id=device)
 
     from trex_amd import SankoffEngine
+    from trex_amd.distributed import shard_bounds
 
-    B, n, L, Q, tau = args.trees_per_gpu, args.taxa, args.sites, args.states, args.tau
-    ch, plan, leaves, cost = make_inputs(torch, device, B, n, L, Q, rank)
+    n, L, Q, tau = args.taxa, args.sites, args.states, args.tau
+    lo, hi = shard_bounds(args.trees, rank, world)
+    B = hi - lo
+    ch, plan, leaves, cost = make_inputs(torch, device, args.trees, n, L, Q, lo, hi)
     eng = SankoffEngine(plan, L, Q, device)
     step = Step(torch, eng, leaves, cost, tau)
     red = torch.zeros(Q * Q + 1, dtype=torch.float32, device=device)
@@ -505,8 +630,8 @@ def main():
         el = float(t.item())
 
     n_int = n - 1
-    units_per_rank = B * L * n_int * Q
-    value = units_per_rank * world * args.steps / el
+    units = args.trees * L * n_int * Q  # the whole batch, all ranks
+    value = units * args.steps / el
 
     # per-kernel device time (HIP events) -> roofline of the step's kernel
     kt = time_kernels(torch, step)
@@ -551,30 +676,37 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (random coalescent topologies, iid uniform leaf states, C = 1 - I)",
-        "config": {"workload": f"C4 shard per GPU: {B} random {n}-taxa topologies x {L} sites x "
-                               f"{Q} states, softmin tau={tau} fwd (DP table written) + grad; "
-                               f"global batch {B * world} trees"
+        "config": {"workload": f"C4: {args.trees} random {n}-taxa topologies x {L} sites x "
+                               f"{Q} states, softmin tau={tau} fwd (DP table written) + grad, "
+                               f"split over {world} GPU(s) ({B} trees on rank 0)"
                                + ("; RCCL all-reduce of [dC, loss] per step, overlapped with "
                                   "the next step" if world > 1 else ""),
-                   "trees_per_gpu": B, "taxa": n, "sites": L, "states": Q, "tau": tau,
-                   "hipgraph": use_graph, "parallelism": f"tree-batch x{world}"},
+                   "trees": args.trees, "trees_rank0": B, "taxa": n, "sites": L, "states": Q,
+                   "tau": tau, "hipgraph": use_graph, "parallelism": f"tree-batch x{world}"},
         "roofline": roofline,
     }
     if rank == 0 and world == 1:
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        hinfo, threads = host_cpu()
+        threads = args.cpu_threads or threads
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(ch, leaves.cpu().numpy(), cost.cpu().numpy(),
                                                   tau, L, n, Q, threads)
+            result["cpu_baseline"]["host"] = hinfo
+        if not args.no_shard:
+            result["c4_shard"] = shard_line(torch, device, ch, leaves, cost, tau, L, Q, n,
+                                            min(128, B))
         if not args.no_c2:
             result["c2"] = c2_line(torch, device, args, threads)
         if not args.no_c3:
             result["c3"] = c3_line(torch, device, threads)
         if not args.no_c5:
             result["c5"] = c5_line(torch, device)
+            torch.cuda.empty_cache()
+            result["c5_f32"] = c5_line(torch, device, gemm="f32")
         if not args.no_nk:
             result["nk"] = nk_line(torch, device)
         if not args.no_ragged:

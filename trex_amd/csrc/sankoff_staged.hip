@@ -134,6 +134,44 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
       hi = offs[s * kSW + wv + 1];
     }
   };
+  // ... and, when they fit (<= 64 stages and steps), this wave's step words
+  // themselves: lane t holds the wave's t-th step (stages in order), read
+  // with v_readlane -- no scalar load (and lgkmcnt wait) on the chain
+  int vbase = 0, sx = 0, sy = 0, sz = 0, sw = 0;
+  bool regsteps;
+  {
+    const int cnt = vhi - vlo;  // 0 in lanes >= S
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int t = __shfl_up(incl, off, kWave);
+      if (lane >= off) incl += t;
+    }
+    vbase = incl - cnt;
+    const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+    regsteps = S <= kWave && total <= kWave;
+    if (regsteps) {
+      int k = -1;
+      for (int s2 = 0; s2 < S; ++s2) {
+        const int b = __builtin_amdgcn_readlane(vbase, s2);
+        const int lo = __builtin_amdgcn_readlane(vlo, s2);
+        const int c = __builtin_amdgcn_readlane(vhi, s2) - lo;
+        if (lane >= b && lane < b + c) k = lo + lane - b;
+      }
+      if (k >= 0) {
+        // (regions are 4-byte aligned only: four dword loads)
+        const int* e = A.staged + (size_t)tree * A.stride + 4 * k;
+        sx = e[0];
+        sy = e[1];
+        sz = e[2];
+        sw = e[3];
+      }
+    }
+  }
+  auto reg_step = [&](int t) {
+    return I4{__builtin_amdgcn_readlane(sx, t), __builtin_amdgcn_readlane(sy, t),
+              __builtin_amdgcn_readlane(sz, t), __builtin_amdgcn_readlane(sw, t)};
+  };
   const uint32_t rowbytes = (uint32_t)L * Q * 4;
   const uint32_t treebytes = (uint32_t)ni * rowbytes;
   const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * ni * L * Q, treebytes);
@@ -142,8 +180,28 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
   const int lgrp = grp < SPW ? grp : 0;
   STAGE_STAMP(0);
 
+  // G = 4 with exact leaf weights: every wave keeps the leaf coefficients of
+  // its lane in registers instead of reading the LDS tables on the chain:
+  // crow[j] = C[i][j] (leaf message), sentm = message of the all-1e5 row,
+  // ikx[j] / wm[j] = adjoint factor of a present / missing leaf state for
+  // accumulator slot j (wm: the all-1e5 row's weights per unit cotangent)
+  constexpr bool REGLEAF = G == 4 && LFAST;
+  float crow[G], ikx[G], wm[G], sentm = 0.0f;
+  if constexpr (REGLEAF) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int col = acc_col<G, MODE>(w.i, j);
+      crow[j] = (w.pad || j >= Q) ? INFINITY : A.cost[w.i * Q + j];
+      const float cc = (w.pad || col >= Q) ? 0.0f : A.cost[w.i * Q + col];
+      ikx[j] = (w.pad || col >= Q) ? 0.0f : (MODE == kSoftK ? fast_exp2((cc - cf.cmin) * a) : 1.0f);
+      wm[j] = 0.0f;
+    }
+    sentm = wmsg<G, MODE>(cf, X, w, a, bcoef, kSentinel);
+    if constexpr (BWD) (void)wadj<G, MODE>(cf, X, w, a, kSentinel, 1.0f, wm);
+  }
+
   // ---- prologue: leaf tables (wave 0), leaf tile, (adjoint only) D rows ----
-  if (wv == 0) {
+  if (!REGLEAF && wv == 0) {
     const float sent = wmsg<G, MODE>(cf, X, w, a, bcoef, kSentinel);
     if (grp == 0) {
       for (int code = 0; code < Q; ++code) {
@@ -177,10 +235,16 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
     for (int s = 0; s < S; ++s) {
       int lo, hi;
       stage_range(s, lo, hi);
-      I4 nxt = load_step(prog, lo < hi ? lo : 0);
+      const int sb = __builtin_amdgcn_readlane(vbase, s < kWave ? s : 0) - lo;
+      I4 nxt = regsteps ? I4{0, 0, 0, 0} : load_step(prog, lo < hi ? lo : 0);
       for (int k = lo; k < hi; ++k) {
-        const I4 stp = nxt;
-        if (k + 1 < hi) nxt = load_step(prog, k + 1);
+        I4 stp;
+        if (regsteps) {
+          stp = reg_step(sb + k);
+        } else {
+          stp = nxt;
+          if (k + 1 < hi) nxt = load_step(prog, k + 1);
+        }
         float dv = 0.0f;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -189,7 +253,11 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
           float m;
           if (kind == kKindLeaf) {
             const int code = lleaf[(desc & 0xFFFF) * SPW + lgrp];
-            if constexpr (LFAST) {
+            if constexpr (REGLEAF) {
+              m = sentm;
+#pragma unroll
+              for (int j = 0; j < G; ++j) m = (code == j && j < Q) ? crow[j] : m;  // code Q: missing
+            } else if constexpr (LFAST) {
               m = tab[code * G + w.i];
             } else {
               m = wmsg<G, MODE>(cf, X, w, a, bcoef, code == w.i ? 0.0f : kSentinel);
@@ -197,7 +265,10 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
           } else if (kind == kKindInt) {
             m = wmsg<G, MODE>(cf, X, w, a, bcoef, dsl[(desc & 0xFFFF) * kWave + lane]);
           } else {
-            m = tab[Q * G + w.i];
+            if constexpr (REGLEAF)
+              m = sentm;
+            else
+              m = tab[Q * G + w.i];
           }
           dv = (c == 0) ? m : dv + m;
         }
@@ -261,10 +332,16 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
     for (int s = S - 1; s >= 0; --s) {
       int lo, hi;
       stage_range(s, lo, hi);
-      I4 nxt = load_step(prog, lo < hi ? hi - 1 : 0);
+      const int sb = __builtin_amdgcn_readlane(vbase, s < kWave ? s : 0) - lo;
+      I4 nxt = regsteps ? I4{0, 0, 0, 0} : load_step(prog, lo < hi ? hi - 1 : 0);
       for (int k = hi - 1; k >= lo; --k) {
-        const I4 stp = nxt;
-        if (k > lo) nxt = load_step(prog, k - 1);
+        I4 stp;
+        if (regsteps) {
+          stp = reg_step(sb + k);
+        } else {
+          stp = nxt;
+          if (k > lo) nxt = load_step(prog, k - 1);
+        }
         if (stp.w & kStepUnreached) continue;
         const int row = stp.x & 0xFFFF;
         const float g = gsl[row * kWave + lane];
@@ -287,6 +364,17 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
           if (kind == kKindLeaf) {
             const int code = lleaf[(desc & 0xFFFF) * SPW + lgrp];
             bool onehot = false;
+            if constexpr (REGLEAF) {
+              // present state: dC[i][code] += g_i (/ K[i][code]); missing
+              // (all-1e5 row): g_i times that row's weights
+              const float gm = code == Q ? g : 0.0f;
+#pragma unroll
+              for (int j = 0; j < G; ++j) {
+                const bool hit = code != Q && acc_col<G, MODE>(w.i, j) == code;
+                acc[j] = fmaf(hit ? g : gm, hit ? ikx[j] : wm[j], acc[j]);
+              }
+              continue;
+            }
             if constexpr (LFAST) onehot = !__any(active && code == Q);
             if (onehot) {
               // exact leaf weights are one-hot: dC[i][code] += g_i (/ K[i][code])
@@ -294,7 +382,7 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
               if constexpr (MODE == kSoftK) t = g * itab[code * G + w.i];
               if (w.pad) t = 0.0f;
 #pragma unroll
-              for (int j = 0; j < G; ++j) acc[j] += (code == j) ? t : 0.0f;
+              for (int j = 0; j < G; ++j) acc[j] += (code == acc_col<G, MODE>(w.i, j)) ? t : 0.0f;
             } else {
               (void)wadj<G, MODE>(cf, X, w, a, code == w.i ? 0.0f : kSentinel, g, acc);
             }
@@ -304,7 +392,12 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
             if (desc & kStepAccumulate) gc += gsl[cs];
             gsl[cs] = gc;
           } else {
-            (void)wadj<G, MODE>(cf, X, w, a, kSentinel, g, acc);
+            if constexpr (REGLEAF) {
+#pragma unroll
+              for (int j = 0; j < G; ++j) acc[j] = fmaf(g, wm[j], acc[j]);
+            } else {
+              (void)wadj<G, MODE>(cf, X, w, a, kSentinel, g, acc);
+            }
           }
         }
       }
@@ -332,7 +425,8 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
         for (int gq = 1; gq < SPW; ++gq) t += __shfl(v, w.i + gq * G, kWave);
       }
       if constexpr (MODE == kSoftK) t *= (double)cf.row[j];
-      if (grp == 0 && !w.pad && j < Q) red[wv * Q2 + w.i * Q + j] = t;
+      const int col = acc_col<G, MODE>(w.i, j);
+      if (grp == 0 && !w.pad && col < Q) red[wv * Q2 + w.i * Q + col] = t;
     }
     lds_barrier();
     const int nb = A.B * A.tiles;
@@ -425,33 +519,16 @@ template <int G, bool SOFT, int PHASE>
 __global__ __launch_bounds__(kSW* kWave, staged_min_waves<G>()) void sankoff_staged_kernel(SArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int Q = A.Q;
-  const int i = (threadIdx.x % kWave) % G;  // G = 20 does not divide 64
-  const bool pad = i >= Q;
-  WCoef<G> cf;
-  float lmin = INFINITY, lmax = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    const bool ok = !pad && j < Q;
-    cf.row[j] = ok ? A.cost[i * Q + j] : INFINITY;
-    cf.col[j] = ok ? A.cost[j * Q + i] : INFINITY;
-    if (ok) {
-      lmin = fminf(lmin, cf.row[j]);
-      lmax = fmaxf(lmax, cf.row[j]);
-    }
-  }
-  cf.cmin = uniform(wave_minf(lmin));
-  const float cmax = uniform(wave_maxf(lmax));
+  const int i = (threadIdx.x % kWave) % G;
+  float cmin, cmax;
+  cost_range<G>(A.cost, Q, i, cmin, cmax);
   if constexpr (!SOFT) {
-    staged_dispatch_leaf<G, kHard, PHASE>(A, cf, cmax, lds);
-  } else if (use_ktrick(cf.cmin, cmax, A.a)) {
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      cf.row[j] = (!pad && j < Q) ? fast_exp2((cf.cmin - cf.row[j]) * A.a) : 0.0f;
-      cf.col[j] = (!pad && j < Q) ? fast_exp2((cf.cmin - cf.col[j]) * A.a) : 0.0f;
-    }
-    staged_dispatch_leaf<G, kSoftK, PHASE>(A, cf, cmax, lds);
+    staged_dispatch_leaf<G, kHard, PHASE>(A, make_coefs<G, kHard>(A.cost, Q, i, cmin, A.a), cmax, lds);
+  } else if (use_ktrick(cmin, cmax, A.a)) {
+    staged_dispatch_leaf<G, kSoftK, PHASE>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a), cmax, lds);
   } else {
-    staged_dispatch_leaf<G, kSoftDirect, PHASE>(A, cf, cmax, lds);
+    staged_dispatch_leaf<G, kSoftDirect, PHASE>(A, make_coefs<G, kSoftDirect>(A.cost, Q, i, cmin, A.a), cmax,
+                                    lds);
   }
 }
 

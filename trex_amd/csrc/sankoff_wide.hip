@@ -243,7 +243,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
             if constexpr (MODE == kSoftK) t = g * itab[code * G + w.i];
             if (w.pad) t = 0.0f;
 #pragma unroll
-            for (int j = 0; j < G; ++j) acc[j] += (code == j) ? t : 0.0f;
+            for (int j = 0; j < G; ++j) acc[j] += (code == acc_col<G, MODE>(w.i, j)) ? t : 0.0f;
           } else {
             (void)wadj<G, MODE>(cf, X, w, a, code == w.i ? 0.0f : kSentinel, g, acc);
           }
@@ -271,7 +271,8 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
       double s = v;  // group 0 sums the groups in order
 #pragma unroll
       for (int gq = 1; gq < SPW; ++gq) s += __shfl(v, w.i + gq * G, kWave);
-      if (grp == 0 && !w.pad && j < Q) A.part_dc[(size_t)(w.i * Q + j) * nb + blockIdx.x] = s;
+      const int col = acc_col<G, MODE>(w.i, j);
+      if (grp == 0 && !w.pad && col < Q) A.part_dc[(size_t)(w.i * Q + col) * nb + blockIdx.x] = s;
     }
   }
 }
@@ -292,32 +293,15 @@ __global__ __launch_bounds__(kWave) void sankoff_wide_kernel(WArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int Q = A.Q;
   const int i = threadIdx.x % G;
-  const bool pad = i >= Q;
-  WCoef<G> cf;
-  float lmin = INFINITY, lmax = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    const bool ok = !pad && j < Q;
-    cf.row[j] = ok ? A.cost[i * Q + j] : INFINITY;
-    cf.col[j] = ok ? A.cost[j * Q + i] : INFINITY;
-    if (ok) {
-      lmin = fminf(lmin, cf.row[j]);
-      lmax = fmaxf(lmax, cf.row[j]);
-    }
-  }
-  cf.cmin = uniform(wave_minf(lmin));
-  const float cmax = uniform(wave_maxf(lmax));
+  float cmin, cmax;
+  cost_range<G>(A.cost, Q, i, cmin, cmax);
   if constexpr (!SOFT) {
-    wide_dispatch_leaf<G, kHard, PHASE>(A, cf, cmax, lds);
-  } else if (use_ktrick(cf.cmin, cmax, A.a)) {
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      cf.row[j] = (!pad && j < Q) ? fast_exp2((cf.cmin - cf.row[j]) * A.a) : 0.0f;
-      cf.col[j] = (!pad && j < Q) ? fast_exp2((cf.cmin - cf.col[j]) * A.a) : 0.0f;
-    }
-    wide_dispatch_leaf<G, kSoftK, PHASE>(A, cf, cmax, lds);
+    wide_dispatch_leaf<G, kHard, PHASE>(A, make_coefs<G, kHard>(A.cost, Q, i, cmin, A.a), cmax, lds);
+  } else if (use_ktrick(cmin, cmax, A.a)) {
+    wide_dispatch_leaf<G, kSoftK, PHASE>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a), cmax, lds);
   } else {
-    wide_dispatch_leaf<G, kSoftDirect, PHASE>(A, cf, cmax, lds);
+    wide_dispatch_leaf<G, kSoftDirect, PHASE>(A, make_coefs<G, kSoftDirect>(A.cost, Q, i, cmin, A.a), cmax,
+                                    lds);
   }
 }
 

@@ -75,15 +75,115 @@ struct WCoef {
   float cmin;
 };
 
+// G = 4, factored softmin (C2 / C4-shaped DNA on small grids): the quad's
+// exchanges are xor quad-permutations applied as DPP operands, and lane i
+// keeps its coefficients and dC accumulators in xor order: row[p] =
+// K[i][i^p], col[p] = K[i^p][i], acc[p] = dC[i][i^p] (xor_perm_coefs at
+// kernel start; acc_col maps back).  No broadcast copies of the quad.
+template <int G, int MODE>
+__host__ __device__ constexpr bool xor_perm() {
+  return G == 4 && MODE == kSoftK;
+}
+template <int G, int MODE>
+__device__ __forceinline__ int acc_col(int i, int j) {
+  if constexpr (xor_perm<G, MODE>()) return i ^ j;
+  return j;
+}
+template <int P>
+__device__ __forceinline__ float qx(float v) {  // lane i of a quad gets v of lane i ^ P
+  constexpr int ctrl = P == 1 ? 0xB1 : P == 2 ? 0x4E : 0x1B;
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float sel4(const float (&v)[4], int k) {
+  return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3];
+}
+
 struct WLane {
   int lane, i, gbase;
   bool pad;  // state i >= Q
 };
 
+// wave-uniform min / max over the cost matrix (every lane scans its row)
+template <int G>
+__device__ __forceinline__ void cost_range(const float* cost, int Q, int i, float& cmin,
+                                           float& cmax) {
+  float lmin = INFINITY, lmax = -INFINITY;
+  if (i < Q) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      if (j < Q) {
+        const float c = cost[i * Q + j];
+        lmin = fminf(lmin, c);
+        lmax = fmaxf(lmax, c);
+      }
+    }
+  }
+  cmin = uniform(wave_minf(lmin));
+  cmax = uniform(wave_maxf(lmax));
+}
+
+template <int G>
+__device__ __forceinline__ void xor_perm_coefs(WCoef<G>& cf, int i);
+
+// lane i's row / column of C (kHard, kSoftDirect) or of K = exp(-(C - cmin) /
+// tau) (kSoftK; xor order for G = 4).  Built inside each mode's branch so the
+// modes' register lifetimes never overlap (one kernel holds all of them)
+template <int G, int MODE>
+__device__ __forceinline__ WCoef<G> make_coefs(const float* cost, int Q, int i, float cmin,
+                                               float a) {
+  WCoef<G> cf;
+  const bool pad = i >= Q;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const bool ok = !pad && j < Q;
+    const float r = ok ? cost[i * Q + j] : INFINITY;
+    const float c = ok ? cost[j * Q + i] : INFINITY;
+    if constexpr (MODE == kSoftK) {
+      cf.row[j] = ok ? fast_exp2((cmin - r) * a) : 0.0f;
+      cf.col[j] = ok ? fast_exp2((cmin - c) * a) : 0.0f;
+    } else {
+      cf.row[j] = r;
+      cf.col[j] = c;
+    }
+  }
+  cf.cmin = cmin;
+  if constexpr (MODE == kSoftK) xor_perm_coefs<G>(cf, i);
+  return cf;
+}
+
+template <int G>
+__device__ __forceinline__ void xor_perm_coefs(WCoef<G>& cf, int i) {
+  if constexpr (G == 4) {
+    float r[4], c[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      r[p] = sel4(cf.row, i ^ p);
+      c[p] = sel4(cf.col, i ^ p);
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      cf.row[p] = r[p];
+      cf.col[p] = c[p];
+    }
+  }
+}
+
 // message to parent state i:  min_j / smin_j (C[i][j] + D[j])   (sankoff.py:67-68)
 template <int G, int MODE>
 __device__ __forceinline__ float wmsg(const WCoef<G>& cf, float* X, const WLane& w, float a,
                                       float bcoef, float D) {
+  if constexpr (xor_perm<G, MODE>()) {
+    (void)X;
+    const float Dv = w.pad ? INFINITY : D;
+    float md = fminf(Dv, qx<1>(Dv));
+    md = fminf(md, qx<2>(md));
+    const float u = w.pad ? 0.0f : fast_exp2((md - D) * a);
+    float s = cf.row[0] * u;
+    s = fmaf(cf.row[1], qx<1>(u), s);
+    s = fmaf(cf.row[2], qx<2>(u), s);
+    s = fmaf(cf.row[3], qx<3>(u), s);
+    return fmaf(-bcoef, fast_log2(s), md + cf.cmin);
+  }
   float d[G];
   xchg<G>(X, w.lane, w.gbase, w.pad ? INFINITY : D, d);
   if constexpr (MODE == kHard) {
@@ -120,6 +220,29 @@ __device__ __forceinline__ float wmsg(const WCoef<G>& cf, float* X, const WLane&
 template <int G, int MODE>
 __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane& w, float a,
                                       float D, float g, float (&acc)[G]) {
+  if constexpr (xor_perm<G, MODE>()) {
+    (void)X;
+    const float Dv = w.pad ? INFINITY : D;
+    float md = fminf(Dv, qx<1>(Dv));
+    md = fminf(md, qx<2>(md));
+    const float u = w.pad ? 0.0f : fast_exp2((md - D) * a);
+    const float u1 = qx<1>(u), u2 = qx<2>(u), u3 = qx<3>(u);
+    float s = cf.row[0] * u;
+    s = fmaf(cf.row[1], u1, s);
+    s = fmaf(cf.row[2], u2, s);
+    s = fmaf(cf.row[3], u3, s);
+    const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(s);
+    acc[0] = fmaf(r, u, acc[0]);
+    acc[1] = fmaf(r, u1, acc[1]);
+    acc[2] = fmaf(r, u2, acc[2]);
+    acc[3] = fmaf(r, u3, acc[3]);
+    // gc_i = u_i sum_q K[i^q][i] r_{i^q}
+    float t = cf.col[0] * r;
+    t = fmaf(cf.col[1], qx<1>(r), t);
+    t = fmaf(cf.col[2], qx<2>(r), t);
+    t = fmaf(cf.col[3], qx<3>(r), t);
+    return u * t;
+  }
   float d[G];
   xchg<G>(X, w.lane, w.gbase, w.pad ? INFINITY : D, d);
   float rr[G];
@@ -158,22 +281,43 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
     for (int p = 0; p < G; ++p) gc += (cf.col[p] + D == mm[p]) ? rr[p] : 0.0f;
     return gc;
   } else {
-    float x[G];
+    // per-row stabilised softmin (rare: range(C)/tau > 40); computed in
+    // place in d[] and, for G > 4, the parents' r / mn streamed from the
+    // exchange buffers: this mode's transients set the register budget of
+    // the whole kernel
     float mn = INFINITY;
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      x[j] = cf.row[j] + d[j];
-      mn = fminf(mn, x[j]);
+      d[j] = cf.row[j] + d[j];
+      mn = fminf(mn, d[j]);
     }
-    float e[G];
     float s = 0.0f;
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      e[j] = fast_exp2((mn - x[j]) * a);
-      s += e[j];
+      d[j] = fast_exp2((mn - d[j]) * a);
+      s += d[j];
     }
     const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(s);
-    axpy<G>(acc, r, e);
+    axpy<G>(acc, r, d);
+    if constexpr (G > 4) {
+      float* xr = X + 2 * kWave;
+      float* xm = X + 3 * kWave;
+      xr[w.lane] = r;
+      xm[w.lane] = w.pad ? 0.0f : mn;
+      wave_sync();
+      float gc = 0.0f;
+#pragma unroll
+      for (int t = 0; t < G / 4; ++t) {
+        const float4 rv = reinterpret_cast<const float4*>(xr + w.gbase)[t];
+        const float4 mv = reinterpret_cast<const float4*>(xm + w.gbase)[t];
+        gc += rv.x * fast_exp2((mv.x - (cf.col[4 * t] + D)) * a);
+        gc += rv.y * fast_exp2((mv.y - (cf.col[4 * t + 1] + D)) * a);
+        gc += rv.z * fast_exp2((mv.z - (cf.col[4 * t + 2] + D)) * a);
+        gc += rv.w * fast_exp2((mv.w - (cf.col[4 * t + 3] + D)) * a);
+      }
+      wave_sync();
+      return gc;
+    }
     float mm[G];
     xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
     xchg<G>(X + 3 * kWave, w.lane, w.gbase, w.pad ? 0.0f : mn, mm);
