@@ -53,3 +53,14 @@ for j in list(range(1, 8)) + [10] + list(range(11, 17)) + [19]:
     prev = j
 tot = t[:, 19] - t[:, 0]
 print(f"{'per-WG total':14s} mean {tot.mean():8.0f}  min {tot.min():8d}  max {tot.max():8d}")
+
+rt = np.zeros((4096, 2), np.uint64)
+f2 = lib().trex_debug_stage_rt
+f2.argtypes = [ctypes.c_void_p]
+assert f2(rt.ctypes.data) == 0
+r = rt[:nwg].astype(np.int64) * 10  # ns
+r0 = r[:, 0].min()
+st, en = r[:, 0] - r0, r[:, 1] - r0
+print("realtime (ns): start min/median/max", st.min(), int(np.median(st)), st.max(),
+      " end min/median/max", en.min(), int(np.median(en)), en.max())
+print("per-WG lifetime ns mean", int((en - st).mean()), "kernel span (first start -> last end)", en.max())

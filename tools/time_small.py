@@ -31,13 +31,15 @@ CONFIGS = {
 }
 
 
-def replay_us(fn, n=300):
+def replay_us(fn, n=100, per_graph=10):
+    """GPU time per step: graphs of per_graph steps (amortises the launch)."""
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        fn()
+        for _ in range(per_graph):
+            fn()
     for _ in range(10):
         g.replay()
     torch.cuda.synchronize()
@@ -47,7 +49,7 @@ def replay_us(fn, n=300):
         for _ in range(n):
             g.replay()
         torch.cuda.synchronize()
-        best.append((time.perf_counter() - t0) / n * 1e6)
+        best.append((time.perf_counter() - t0) / n / per_graph * 1e6)
     return min(best)
 
 

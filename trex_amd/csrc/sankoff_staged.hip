@@ -62,6 +62,12 @@ struct SArgs {
 // diagnostic build (tools/build_diag.sh): wave 0 of each of the first 4096
 // workgroups stamps s_memtime at phase boundaries
 __device__ unsigned long long g_stage_t[4096][20];
+__device__ unsigned long long g_stage_rt[4096][2];  // s_memrealtime (100 MHz) at start / end
+#define STAGE_RT(j)                                                              \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                                 \
+      g_stage_rt[blockIdx.x][j] = __builtin_amdgcn_s_memrealtime();            \
+  } while (0)
 #define STAGE_STAMP(j)                                                         \
   do {                                                                         \
     if (threadIdx.x == 0 && blockIdx.x < 4096 && (j) < 20)                     \
@@ -70,6 +76,9 @@ __device__ unsigned long long g_stage_t[4096][20];
 #else
 #define STAGE_STAMP(j) \
   do {                 \
+  } while (0)
+#define STAGE_RT(j) \
+  do {              \
   } while (0)
 #endif
 
@@ -179,6 +188,7 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
   const int voff = (active && !w.pad) ? (site * Q + w.i) * 4 : 0x7FFFFFF0;
   const int lgrp = grp < SPW ? grp : 0;
   STAGE_STAMP(0);
+  STAGE_RT(0);
 
   // G = 4 with exact leaf weights: every wave keeps the leaf coefficients of
   // its lane in registers instead of reading the LDS tables on the chain:
@@ -348,13 +358,7 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
         if (want_marg)
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), rmg, voff, row * rowbytes, 0);
         if (want_anc) {
-          float gg[G];
-          xchg<G>(X, lane, w.gbase, w.pad ? -INFINITY : g, gg);
-          float bv = gg[0];
-          int bi = 0;
-#pragma unroll
-          for (int j = 1; j < G; ++j)
-            if (gg[j] > bv) { bv = gg[j]; bi = j; }
+          const int bi = group_argmax<G>(X, w, w.pad ? -INFINITY : g);
           if (leader) at[(size_t)row * L] = (int8_t)bi;
         }
 #pragma unroll
@@ -381,8 +385,7 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
               float t = g;
               if constexpr (MODE == kSoftK) t = g * itab[code * G + w.i];
               if (w.pad) t = 0.0f;
-#pragma unroll
-              for (int j = 0; j < G; ++j) acc[j] += (code == acc_col<G, MODE>(w.i, j)) ? t : 0.0f;
+              onehot_add<G, MODE>(acc, w.i, code, t);
             } else {
               (void)wadj<G, MODE>(cf, X, w, a, code == w.i ? 0.0f : kSentinel, g, acc);
             }
@@ -438,6 +441,7 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
     }
     STAGE_STAMP(19);
   }
+  STAGE_RT(1);
 
   // ---- last workgroup: fixed-order sums of every item's partials.
   // Partials are written and read at device scope (sc1) and each wave waits
@@ -572,6 +576,9 @@ size_t staged_lds_g(int ni, int nl, int Q, int phase) {
 #ifdef TREX_STAGED_TIMING
 extern "C" int trex_debug_stage_times(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_t), sizeof(g_stage_t)) == hipSuccess ? 0 : -4;
+}
+extern "C" int trex_debug_stage_rt(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage_rt), sizeof(g_stage_rt)) == hipSuccess ? 0 : -4;
 }
 #endif
 

@@ -77,7 +77,15 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
   float* tab = lds + kXchg;                       // T[code][i]
   float* itab = tab + (Q + 1) * G;                // IK[code][i]
   float* slots = lds + kXchg + wide_tab_floats(G, Q);
-  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (A.n_slots + 1) * kWave);
+  // fused factored softmin: each internal child's stabiliser md per site
+  // group, kept from the forward for the adjoint ([n_int][SPW])
+#ifdef TREX_DIAG_NO_KEEPMD
+  constexpr bool KEEP_MD = false;
+#else
+  constexpr bool KEEP_MD = PHASE == 3 && MODE == kSoftK && G > 4;
+#endif
+  float* mdc = slots + (A.n_slots + 1) * kWave;
+  int8_t* lleaf = reinterpret_cast<int8_t*>(mdc + (size_t)A.n_int * SPW);
 
   // ---- prologue: leaf tables + leaf tile ----
   {
@@ -130,7 +138,13 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
           }
         } else if (kind == kKindInt) {
           const float D = (desc & kChildPrev) ? prev : slots[((desc >> 16) & 0xFF) * kWave + lane];
-          m = wmsg<G, MODE>(cf, X, w, a, bcoef, D);
+          if constexpr (KEEP_MD) {
+            float mdv;
+            m = wmsg<G, MODE>(cf, X, w, a, bcoef, D, &mdv);
+            if (w.i == 0) mdc[(desc & 0xFFFF) * SPW + lgrp] = mdv;
+          } else {
+            m = wmsg<G, MODE>(cf, X, w, a, bcoef, D);
+          }
         } else {
           m = tab[Q * G + w.i];
         }
@@ -220,13 +234,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
       if (want_marg)
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), rmg, voff, row * rowbytes, 0);
       if (want_anc) {
-        float gg[G];
-        xchg<G>(X, lane, w.gbase, w.pad ? -INFINITY : g, gg);
-        float bv = gg[0];
-        int bi = 0;
-#pragma unroll
-        for (int j = 1; j < G; ++j)
-          if (gg[j] > bv) { bv = gg[j]; bi = j; }
+        const int bi = group_argmax<G>(X, w, w.pad ? -INFINITY : g);
         if (leader) at[(size_t)row * L] = (int8_t)bi;
       }
 #pragma unroll
@@ -242,13 +250,17 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
             float t = g;
             if constexpr (MODE == kSoftK) t = g * itab[code * G + w.i];
             if (w.pad) t = 0.0f;
-#pragma unroll
-            for (int j = 0; j < G; ++j) acc[j] += (code == acc_col<G, MODE>(w.i, j)) ? t : 0.0f;
+            onehot_add<G, MODE>(acc, w.i, code, t);
           } else {
             (void)wadj<G, MODE>(cf, X, w, a, code == w.i ? 0.0f : kSentinel, g, acc);
           }
         } else if (kind == kKindInt) {
-          float gc = wadj<G, MODE>(cf, X, w, a, c == 0 ? cd0 : cd1, g, acc);
+          float gc;
+          if constexpr (KEEP_MD)
+            gc = wadj_k_md<G>(cf, X, w, a, c == 0 ? cd0 : cd1, mdc[(desc & 0xFFFF) * SPW + lgrp], g,
+                              acc);
+          else
+            gc = wadj<G, MODE>(cf, X, w, a, c == 0 ? cd0 : cd1, g, acc);
           if (desc & kChildPrev) {
             gnext = gc;
           } else {
@@ -464,9 +476,10 @@ int wide_tiles(int L, int Q) {
   return (L + spw - 1) / spw;
 }
 
-size_t wide_lds_bytes(int n_slots, int nl, int Q) {
+size_t wide_lds_bytes(int n_slots, int nl, int ni, int Q) {
   const int G = wide_group(Q);
-  const size_t b = (size_t)(kXchg + wide_tab_floats(G, Q) + (n_slots + 1) * kWave) * 4 +
+  const size_t b = (size_t)(kXchg + wide_tab_floats(G, Q) + (n_slots + 1) * kWave +
+                            (size_t)ni * (kWave / G)) * 4 +
                    (size_t)nl * (kWave / G);
   return (b + 15) & ~(size_t)15;
 }
@@ -478,7 +491,7 @@ int64_t wide_workspace_bytes(int B, int L, int Q) {
 
 int wide_run(const char* fn, const WideCall& c) {
   const int tiles = wide_tiles(c.L, c.Q);
-  const size_t lds = wide_lds_bytes(c.n_slots, c.nl, c.Q);
+  const size_t lds = wide_lds_bytes(c.n_slots, c.nl, c.ni, c.Q);
   if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
   if ((int64_t)c.B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
   if ((int64_t)c.ni * c.L * c.Q * 4 > 0x7FFFFFF0LL)

@@ -87,7 +87,7 @@ struct WideCall {
 constexpr int kWideMaxQ = 32;
 int wide_group(int Q);
 int wide_tiles(int L, int Q);
-size_t wide_lds_bytes(int n_slots, int nl, int Q);
+size_t wide_lds_bytes(int n_slots, int nl, int ni, int Q);
 int64_t wide_workspace_bytes(int B, int L, int Q);
 int wide_run(const char* fn, const WideCall& c);
 // staged multi-wave kernel (sankoff_staged.hip); staged = the plan's staged

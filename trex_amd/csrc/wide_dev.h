@@ -18,6 +18,7 @@ constexpr int kXchg = 4 * kWave;
 
 __host__ __device__ constexpr int wide_tab_floats(int G, int Q) { return (2 * Q + 1) * G; }
 
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
@@ -171,7 +172,7 @@ __device__ __forceinline__ void xor_perm_coefs(WCoef<G>& cf, int i) {
 // message to parent state i:  min_j / smin_j (C[i][j] + D[j])   (sankoff.py:67-68)
 template <int G, int MODE>
 __device__ __forceinline__ float wmsg(const WCoef<G>& cf, float* X, const WLane& w, float a,
-                                      float bcoef, float D) {
+                                      float bcoef, float D, float* md_out = nullptr) {
   if constexpr (xor_perm<G, MODE>()) {
     (void)X;
     const float Dv = w.pad ? INFINITY : D;
@@ -195,6 +196,7 @@ __device__ __forceinline__ float wmsg(const WCoef<G>& cf, float* X, const WLane&
     float md = d[0];
 #pragma unroll
     for (int j = 1; j < G; ++j) md = fminf(md, d[j]);
+    if (md_out) *md_out = md;
     const float u = w.pad ? 0.0f : fast_exp2((md - D) * a);
     float uu[G];
     xchg<G>(X + kWave, w.lane, w.gbase, u, uu);
@@ -326,6 +328,62 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
     for (int p = 0; p < G; ++p) gc += rr[p] * fast_exp2((mm[p] - (cf.col[p] + D)) * a);
     return gc;
   }
+}
+
+// exact one-hot leaf weight: acc[slot of column code] += t.  G > 4: pairs
+// of slots at once, one-hot(j) = clamp(1 - (code - j)^2) on packed FP32
+// (exact for integer codes; clamp folded into the packed FMA) -- 1.5 VALU
+// per slot instead of a compare, select and add
+__device__ __forceinline__ f2 onehot2(f2 x) {
+  f2 y;
+  asm("v_pk_fma_f32 %0, %1, %1, 1.0 op_sel_hi:[1,1,0] neg_lo:[1,0,0] neg_hi:[1,0,0] clamp"
+      : "=v"(y)
+      : "v"(x));
+  return y;
+}
+template <int G, int MODE>
+__device__ __forceinline__ void onehot_add(float (&acc)[G], int i, int code, float t) {
+  if constexpr (G > 4 && G % 2 == 0) {
+    const float f = (float)code;
+#pragma unroll
+    for (int j = 0; j < G; j += 2)
+      pfma(acc[j], acc[j + 1], pk(t, t), onehot2(pk(f, f) - pk((float)j, (float)(j + 1))));
+  } else {
+#pragma unroll
+    for (int j = 0; j < G; ++j) acc[j] += (code == acc_col<G, MODE>(i, j)) ? t : 0.0f;
+  }
+}
+
+// first-index argmax of the group's values v (lane i holds state i; padded
+// states pass -inf): the group max, then the lowest lane of the group that
+// holds it from a wave ballot -- no G-step compare / select chain
+template <int G>
+__device__ __forceinline__ int group_argmax(float* X, const WLane& w, float v) {
+  float gg[G];
+  xchg<G>(X, w.lane, w.gbase, v, gg);
+  float bv = gg[0];
+#pragma unroll
+  for (int j = 1; j < G; ++j) bv = fmaxf(bv, gg[j]);
+  const unsigned long long hit = __ballot(!w.pad && v == bv);
+  return __builtin_ctzll((hit >> w.gbase) | (1ull << 63));
+}
+
+// wadj for the factored softmin when the child's stabiliser md = min_j D[j]
+// is already known (kept from the fused kernel's forward): no exchange of D
+// and no G-way min -- the same arithmetic, bitwise the same result
+template <int G>
+__device__ __forceinline__ float wadj_k_md(const WCoef<G>& cf, float* X, const WLane& w, float a,
+                                           float D, float md, float g, float (&acc)[G]) {
+  // (min: sites past L read D = 0 in the adjoint, not their forward value;
+  // exact no-op for real sites, md <= D)
+  const float u = w.pad ? 0.0f : fast_exp2(fminf((md - D) * a, 0.0f));
+  float uu[G];
+  xchg<G>(X + kWave, w.lane, w.gbase, u, uu);
+  const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(kdot<G>(cf.row, uu));
+  axpy<G>(acc, r, uu);
+  float rr[G];
+  xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
+  return u * kdot<G>(cf.col, rr);
 }
 
 // Fixed-order sum of n doubles by 256 threads (t = 0..255 of a group that
