@@ -92,7 +92,7 @@ __host__ __device__ constexpr int staged_xchg_floats() {
 }
 
 template <int G, int MODE, int PHASE, bool LFAST>
-__device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, float* lds) {
+__device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf_in, float* lds) {
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
@@ -116,6 +116,9 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
 
   float* X = lds + (G == 4 ? 0 : wv * kXchg);
   float* tab = lds + staged_xchg_floats<G>();  // T[code][i]
+  float* ctab = tab + wide_col_table_offset(G, Q);  // G > 4: lane columns of C / K
+  WCoef<G> cf = cf_in;
+  cf.cl = ctab + (w.i < G ? w.i : 0) * G;
   float* itab = tab + (Q + 1) * G;             // IK[code][i]
   float* dsl = tab + wide_tab_floats(G, Q);    // D of internal row r: dsl[r * 64 + lane]
   float* gsl = dsl + (size_t)ni * kWave;       // cotangents (BWD)
@@ -220,6 +223,7 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
         if constexpr (MODE == kSoftK) itab[code * G + w.i] = w.pad ? 0.0f : fast_exp2((cv - cf.cmin) * a);
       }
       tab[Q * G + w.i] = sent;
+      fill_col_table<G, MODE>(ctab, A.cost, Q, w.i, cf.cmin, a);
     }
   }
   {
@@ -383,7 +387,8 @@ __device__ __forceinline__ void staged_body(const SArgs& A, const WCoef<G>& cf, 
             if (onehot) {
               // exact leaf weights are one-hot: dC[i][code] += g_i (/ K[i][code])
               float t = g;
-              if constexpr (MODE == kSoftK) t = g * itab[code * G + w.i];
+              // (code Q only at sites past L, whose cotangent is 0: IK has no row Q)
+            if constexpr (MODE == kSoftK) t = code < Q ? g * itab[code * G + w.i] : 0.0f;
               if (w.pad) t = 0.0f;
               onehot_add<G, MODE>(acc, w.i, code, t);
             } else {

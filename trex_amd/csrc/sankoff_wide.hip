@@ -52,8 +52,8 @@ struct WArgs {
 // slots [n_slots + 1][64] (n_slots = root cotangent), leaf tile [nl][64/G] i8
 // (exchange helpers, wmsg / wadj: wide_dev.h)
 
-template <int G, int MODE, int PHASE, bool LFAST>
-__device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, float* lds) {
+template <int G, int MODE, int PHASE, bool LFAST, bool SYM>
+__device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in, float* lds) {
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
@@ -75,6 +75,9 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
 
   float* X = lds;
   float* tab = lds + kXchg;                       // T[code][i]
+  float* ctab = tab + wide_col_table_offset(G, Q);  // G > 4: lane columns of C / K
+  WCoef<G> cf = cf_in;
+  cf.cl = ctab + (w.i < G ? w.i : 0) * G;
   float* itab = tab + (Q + 1) * G;                // IK[code][i]
   float* slots = lds + kXchg + wide_tab_floats(G, Q);
   // fused factored softmin: each internal child's stabiliser md per site
@@ -97,6 +100,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
         if constexpr (MODE == kSoftK) itab[code * G + w.i] = w.pad ? 0.0f : fast_exp2((cv - cf.cmin) * a);
       }
       tab[Q * G + w.i] = sent;
+      if constexpr (!SYM) fill_col_table<G, MODE>(ctab, A.cost, Q, w.i, cf.cmin, a);
     }
     const int8_t* lv = A.leaves + (size_t)tree * A.nl * L;
     for (int t = lane; t < A.nl * SPW; t += kWave) {
@@ -248,19 +252,20 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
           if (onehot) {
             // exact leaf weights are one-hot: dC[i][code] += g_i (/ K[i][code])
             float t = g;
-            if constexpr (MODE == kSoftK) t = g * itab[code * G + w.i];
+            // (code Q only at sites past L, whose cotangent is 0: IK has no row Q)
+            if constexpr (MODE == kSoftK) t = code < Q ? g * itab[code * G + w.i] : 0.0f;
             if (w.pad) t = 0.0f;
             onehot_add<G, MODE>(acc, w.i, code, t);
           } else {
-            (void)wadj<G, MODE>(cf, X, w, a, code == w.i ? 0.0f : kSentinel, g, acc);
+            (void)wadj<G, MODE, SYM>(cf, X, w, a, code == w.i ? 0.0f : kSentinel, g, acc);
           }
         } else if (kind == kKindInt) {
           float gc;
           if constexpr (KEEP_MD)
-            gc = wadj_k_md<G>(cf, X, w, a, c == 0 ? cd0 : cd1, mdc[(desc & 0xFFFF) * SPW + lgrp], g,
+            gc = wadj_k_md<G, SYM>(cf, X, w, a, c == 0 ? cd0 : cd1, mdc[(desc & 0xFFFF) * SPW + lgrp], g,
                               acc);
           else
-            gc = wadj<G, MODE>(cf, X, w, a, c == 0 ? cd0 : cd1, g, acc);
+            gc = wadj<G, MODE, SYM>(cf, X, w, a, c == 0 ? cd0 : cd1, g, acc);
           if (desc & kChildPrev) {
             gnext = gc;
           } else {
@@ -269,7 +274,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
             slots[cslot * kWave + lane] = gc;
           }
         } else {
-          (void)wadj<G, MODE>(cf, X, w, a, kSentinel, g, acc);
+          (void)wadj<G, MODE, SYM>(cf, X, w, a, kSentinel, g, acc);
         }
       }
     }
@@ -289,31 +294,47 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf, fl
   }
 }
 
-template <int G, int MODE, int PHASE>
+template <int G, int MODE, int PHASE, bool SYM = false>
 __device__ __forceinline__ void wide_dispatch_leaf(const WArgs& A, const WCoef<G>& cf, float cmax,
                                                    float* lds) {
   const float range = cmax - cf.cmin;
   const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
   if (lfast)
-    wide_body<G, MODE, PHASE, true>(A, cf, lds);
+    wide_body<G, MODE, PHASE, true, SYM>(A, cf, lds);
   else
-    wide_body<G, MODE, PHASE, false>(A, cf, lds);
+    wide_body<G, MODE, PHASE, false, SYM>(A, cf, lds);
 }
 
+#ifndef TREX_WIDE_MINW
+#define TREX_WIDE_MINW 4
+#endif
+// Q = 20 (C3): 4 waves per SIMD (<= 128 VGPRs) for the adjoint-bearing
+// kernels -- 3 334 waves of C3 then fit the chip in one round
+template <int G, int PHASE>
+constexpr int wide_min_blocks() { return (G == 20 && (PHASE & 2)) ? TREX_WIDE_MINW : 1; }
+
 template <int G, bool SOFT, int PHASE>
-__global__ __launch_bounds__(kWave) void sankoff_wide_kernel(WArgs A) {
+__global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_wide_kernel(WArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int Q = A.Q;
   const int i = threadIdx.x % G;
   float cmin, cmax;
-  cost_range<G>(A.cost, Q, i, cmin, cmax);
+  bool sym;
+  cost_range<G>(A.cost, Q, i, cmin, cmax, &sym);
   if constexpr (!SOFT) {
     wide_dispatch_leaf<G, kHard, PHASE>(A, make_coefs<G, kHard>(A.cost, Q, i, cmin, A.a), cmax, lds);
   } else if (use_ktrick(cmin, cmax, A.a)) {
-    wide_dispatch_leaf<G, kSoftK, PHASE>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a), cmax, lds);
+    // symmetric costs (C3's protein matrix; C = 1 - I): K's column i is row
+    // i, a variant without the column registers
+    if (G > 4 && sym)
+      wide_dispatch_leaf<G, kSoftK, PHASE, G != 4>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a),
+                                                   cmax, lds);
+    else
+      wide_dispatch_leaf<G, kSoftK, PHASE>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a), cmax,
+                                           lds);
   } else {
-    wide_dispatch_leaf<G, kSoftDirect, PHASE>(A, make_coefs<G, kSoftDirect>(A.cost, Q, i, cmin, A.a), cmax,
-                                    lds);
+    wide_dispatch_leaf<G, kSoftDirect, PHASE>(A, make_coefs<G, kSoftDirect>(A.cost, Q, i, cmin, A.a),
+                                              cmax, lds);
   }
 }
 

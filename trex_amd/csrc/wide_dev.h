@@ -16,7 +16,12 @@ namespace {
 // (row Q = message of the all-1e5 row) and IK[Q][G] = 1 / K[i][code]
 constexpr int kXchg = 4 * kWave;
 
-__host__ __device__ constexpr int wide_tab_floats(int G, int Q) { return (2 * Q + 1) * G; }
+// leaf message table T[Q + 1][G], IK[Q][G], and for G > 4 the per-lane
+// column table CT[G][G] (CT[i][j] = column i of C / K at row j)
+__host__ __device__ constexpr int wide_tab_floats(int G, int Q) {
+  return (2 * Q + 1) * G + (G > 4 ? G * G : 0);
+}
+__host__ __device__ constexpr int wide_col_table_offset(int G, int Q) { return (2 * Q + 1) * G; }
 
 
 __device__ __forceinline__ void wave_sync() {
@@ -72,7 +77,8 @@ __device__ __forceinline__ float wave_maxf(float v) {
 template <int G>
 struct WCoef {
   float row[G];
-  float col[G];
+  float col[G];        // G = 4 only (G > 4: the LDS table cl, or row when symmetric)
+  const float* cl;     // G > 4: this lane's column of C / K in LDS (wide_col_table)
   float cmin;
 };
 
@@ -107,8 +113,9 @@ struct WLane {
 // wave-uniform min / max over the cost matrix (every lane scans its row)
 template <int G>
 __device__ __forceinline__ void cost_range(const float* cost, int Q, int i, float& cmin,
-                                           float& cmax) {
+                                           float& cmax, bool* sym = nullptr) {
   float lmin = INFINITY, lmax = -INFINITY;
+  bool s = true;
   if (i < Q) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
@@ -116,11 +123,13 @@ __device__ __forceinline__ void cost_range(const float* cost, int Q, int i, floa
         const float c = cost[i * Q + j];
         lmin = fminf(lmin, c);
         lmax = fmaxf(lmax, c);
+        s = s && c == cost[j * Q + i];
       }
     }
   }
   cmin = uniform(wave_minf(lmin));
   cmax = uniform(wave_maxf(lmax));
+  if (sym) *sym = __all(s);
 }
 
 template <int G>
@@ -141,12 +150,13 @@ __device__ __forceinline__ WCoef<G> make_coefs(const float* cost, int Q, int i, 
     const float c = ok ? cost[j * Q + i] : INFINITY;
     if constexpr (MODE == kSoftK) {
       cf.row[j] = ok ? fast_exp2((cmin - r) * a) : 0.0f;
-      cf.col[j] = ok ? fast_exp2((cmin - c) * a) : 0.0f;
+      cf.col[j] = (G == 4 && ok) ? fast_exp2((cmin - c) * a) : 0.0f;
     } else {
       cf.row[j] = r;
-      cf.col[j] = c;
+      cf.col[j] = G == 4 ? c : 0.0f;
     }
   }
+  cf.cl = nullptr;
   cf.cmin = cmin;
   if constexpr (MODE == kSoftK) xor_perm_coefs<G>(cf, i);
   return cf;
@@ -219,7 +229,48 @@ __device__ __forceinline__ float wmsg(const WCoef<G>& cf, float* X, const WLane&
 // adjoint of one child message: acc[j] += g_i w_ij (row i of dC; in the K
 // form the K[i][j] factor is applied once at the end); returns the child's
 // cotangent for state i:  gc_i = sum_p g_p w_pi
+// lane i's column of C (kHard, kSoftDirect) / K (kSoftK) into the LDS
+// table at ct (G > 4; called by the lanes of one group)
 template <int G, int MODE>
+__device__ __forceinline__ void fill_col_table(float* ct, const float* cost, int Q, int i,
+                                               float cmin, float a) {
+  if constexpr (G > 4) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const bool ok = i < Q && j < Q;
+      const float c = ok ? cost[j * Q + i] : INFINITY;
+      ct[i * G + j] = MODE == kSoftK ? (ok ? fast_exp2((cmin - c) * a) : 0.0f) : c;
+    }
+  }
+}
+template <int G, bool SYM>
+__device__ __forceinline__ float ccol(const WCoef<G>& cf, int p) {
+  if constexpr (SYM) return cf.row[p];
+  else if constexpr (G == 4) return cf.col[p];
+  else return cf.cl[p];
+}
+// sum_p column[p] * r[p], the LDS column streamed in float4 chunks
+template <int G, bool SYM>
+__device__ __forceinline__ float kdot_col(const WCoef<G>& cf, const float (&r)[G]) {
+  if constexpr (SYM) {
+    return kdot<G>(cf.row, r);
+  } else if constexpr (G == 4) {
+    return kdot<G>(cf.col, r);
+  } else {
+    f2 acc2 = pk(0.0f, 0.0f);
+#pragma unroll
+    for (int t = 0; t < G / 4; ++t) {
+      const float4 v = reinterpret_cast<const float4*>(cf.cl)[t];
+      acc2 = __builtin_elementwise_fma(pk(v.x, v.y), pk(r[4 * t], r[4 * t + 1]), acc2);
+      acc2 = __builtin_elementwise_fma(pk(v.z, v.w), pk(r[4 * t + 2], r[4 * t + 3]), acc2);
+    }
+    return acc2.x + acc2.y;
+  }
+}
+
+// SYM: the cost matrix is symmetric (so is K): column i of K is row i, and
+// the column registers are never read (the compiler drops them)
+template <int G, int MODE, bool SYM = false>
 __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane& w, float a,
                                       float D, float g, float (&acc)[G]) {
   if constexpr (xor_perm<G, MODE>()) {
@@ -258,7 +309,7 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
     const float r = w.pad ? 0.0f : g * __builtin_amdgcn_rcpf(kdot<G>(cf.row, uu));
     axpy<G>(acc, r, uu);
     xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
-    return u * kdot<G>(cf.col, rr);
+    return u * kdot_col<G, SYM>(cf, rr);
   } else if constexpr (MODE == kHard) {
     float x[G];
     float mn = cf.row[0] + d[0];
@@ -280,7 +331,7 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
     // parent p's x_{p i} = C[p][i] + D_i, bit-identical to lane p's x[i]
     float gc = 0.0f;
 #pragma unroll
-    for (int p = 0; p < G; ++p) gc += (cf.col[p] + D == mm[p]) ? rr[p] : 0.0f;
+    for (int p = 0; p < G; ++p) gc += (ccol<G, SYM>(cf, p) + D == mm[p]) ? rr[p] : 0.0f;
     return gc;
   } else {
     // per-row stabilised softmin (rare: range(C)/tau > 40); computed in
@@ -312,10 +363,10 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
       for (int t = 0; t < G / 4; ++t) {
         const float4 rv = reinterpret_cast<const float4*>(xr + w.gbase)[t];
         const float4 mv = reinterpret_cast<const float4*>(xm + w.gbase)[t];
-        gc += rv.x * fast_exp2((mv.x - (cf.col[4 * t] + D)) * a);
-        gc += rv.y * fast_exp2((mv.y - (cf.col[4 * t + 1] + D)) * a);
-        gc += rv.z * fast_exp2((mv.z - (cf.col[4 * t + 2] + D)) * a);
-        gc += rv.w * fast_exp2((mv.w - (cf.col[4 * t + 3] + D)) * a);
+        gc += rv.x * fast_exp2((mv.x - (ccol<G, SYM>(cf, 4 * t) + D)) * a);
+        gc += rv.y * fast_exp2((mv.y - (ccol<G, SYM>(cf, 4 * t + 1) + D)) * a);
+        gc += rv.z * fast_exp2((mv.z - (ccol<G, SYM>(cf, 4 * t + 2) + D)) * a);
+        gc += rv.w * fast_exp2((mv.w - (ccol<G, SYM>(cf, 4 * t + 3) + D)) * a);
       }
       wave_sync();
       return gc;
@@ -325,7 +376,7 @@ __device__ __forceinline__ float wadj(const WCoef<G>& cf, float* X, const WLane&
     xchg<G>(X + 3 * kWave, w.lane, w.gbase, w.pad ? 0.0f : mn, mm);
     float gc = 0.0f;
 #pragma unroll
-    for (int p = 0; p < G; ++p) gc += rr[p] * fast_exp2((mm[p] - (cf.col[p] + D)) * a);
+    for (int p = 0; p < G; ++p) gc += rr[p] * fast_exp2((mm[p] - (ccol<G, SYM>(cf, p) + D)) * a);
     return gc;
   }
 }
@@ -371,7 +422,7 @@ __device__ __forceinline__ int group_argmax(float* X, const WLane& w, float v) {
 // wadj for the factored softmin when the child's stabiliser md = min_j D[j]
 // is already known (kept from the fused kernel's forward): no exchange of D
 // and no G-way min -- the same arithmetic, bitwise the same result
-template <int G>
+template <int G, bool SYM = false>
 __device__ __forceinline__ float wadj_k_md(const WCoef<G>& cf, float* X, const WLane& w, float a,
                                            float D, float md, float g, float (&acc)[G]) {
   // (min: sites past L read D = 0 in the adjoint, not their forward value;
@@ -383,7 +434,7 @@ __device__ __forceinline__ float wadj_k_md(const WCoef<G>& cf, float* X, const W
   axpy<G>(acc, r, uu);
   float rr[G];
   xchg<G>(X + 2 * kWave, w.lane, w.gbase, r, rr);
-  return u * kdot<G>(cf.col, rr);
+  return u * kdot_col<G, SYM>(cf, rr);
 }
 
 // Fixed-order sum of n doubles by 256 threads (t = 0..255 of a group that
