@@ -41,7 +41,10 @@ extern "C" {
 /* flags for trex_sankoff_fwd / trex_sankoff_bwd */
 #define TREX_FLAG_HARD_ROOT 1u  /* tau>0: site score = min(D_root), not smin */
 
-/* plan layout constants (see trex_plan_build) */
+/* plan layout constants (see trex_plan_build).  A plan holds, after the
+ * header, the forward steps [B][n_int][4], the backtrack entries
+ * [B][n_int][2] and the staged (multi-wave) program of every tree (the
+ * small-grid kernel, sankoff_staged.hip); trex_plan_ints sizes all of it. */
 #define TREX_PLAN_HEADER_INTS 16
 
 const char* trex_last_error(void);
@@ -88,7 +91,8 @@ int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
  *            rows; a lane's Q states are one 8/12/16-byte access for Q <= 4,
  *            a lane group's row for the lane-per-state kernels, Q > 4)
  *   site_score fp32 [B][L] or NULL;  tree_score fp32 [B] (required)
- * Q > 32 returns TREX_E_UNSUPPORTED.
+ * Q up to 64 (codon alphabets; leaf codes and ancestral states are int8);
+ * Q > 64 returns TREX_E_UNSUPPORTED.
  * ---------------------------------------------------------------------- */
 int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
                      const float* cost, int B, int L, int n_all, int Q, float tau,
@@ -326,8 +330,11 @@ int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, int Q, floa
  * Packed tensors: leaves int8 [sum n_leaves_b L_b] (tree b: [n_leaves_b][L_b]);
  * dp / marginals f32 [sum n_int_b L_b][Q] (tree b: [n_int_b][L_b][Q]);
  * site_score f32 [sum L_b]; anc_states int8 [sum n_int_b L_b];
- * tree_score / d_tree_score [B].  Q <= 4.  phase: 1 forward, 2 adjoint,
- * 3 fused (same semantics as trex_sankoff_fwd / _bwd / _fwd_bwd per tree).
+ * tree_score / d_tree_score [B].  Q <= 64 (Q > 4: the state-parallel
+ * kernel, each 64-site item split over ceil(64 / sites-per-wave) waves; its
+ * workspace is sized by trex_ragged_workspace_bytes(items, Q)).  phase: 1
+ * forward, 2 adjoint, 3 fused (same semantics as trex_sankoff_fwd / _bwd /
+ * _fwd_bwd per tree).
  * ---------------------------------------------------------------------- */
 int64_t trex_ragged_plan_ints(int B, const int32_t* n_all, const int32_t* L);
 int trex_ragged_plan_build(const int32_t* children, const int32_t* n_all, const int32_t* L, int B,

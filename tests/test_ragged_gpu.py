@@ -1,6 +1,9 @@
 """Ragged tree batches (mixed n_all_b / L_b in one launch) vs the oracle and
 vs the uniform engine run tree by tree.
 
+Q <= 4 runs the lane-per-site kernel, Q = 5 / 20 / 61 the state-parallel
+one (each 64-site item split over ceil(64 / sites-per-wave) waves).
+
 Bars: hard path bit-exact (dp, per-tree / per-site scores, trex backtrack);
 per-tree scores and dp also bitwise equal to a uniform SankoffEngine on the
 same tree (same kernel arithmetic); d_cost rtol 1e-6 (hard) / 1e-5 (softmin)
@@ -38,7 +41,7 @@ def _ref(chs, leaves, cost, tau, dts):
             for b, (c, lv) in enumerate(zip(chs, leaves))]
 
 
-@pytest.mark.parametrize("Q", [2, 3, 4])
+@pytest.mark.parametrize("Q", [2, 3, 4, 5, 20, 61])
 def test_ragged_hard_matches_oracle_and_uniform(device, Q):
     chs, leaves = _batch(Q, seed=Q, missing=0.05)
     plan = RaggedTreePlan(chs, [L for _, L in SIZES])
@@ -71,9 +74,9 @@ def test_ragged_hard_matches_oracle_and_uniform(device, Q):
                                    rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("Q", [4, 20])
 @pytest.mark.parametrize("tau", [0.3, 1.0])
-def test_ragged_softmin_fused_vs_oracle(device, tau):
-    Q = 4
+def test_ragged_softmin_fused_vs_oracle(device, tau, Q):
     chs, leaves = _batch(Q, seed=40)
     plan = RaggedTreePlan(chs, [L for _, L in SIZES])
     eng = RaggedSankoffEngine(plan, Q, device)
@@ -96,8 +99,8 @@ def test_ragged_softmin_fused_vs_oracle(device, tau):
     assert torch.equal(mg, mg2)
 
 
-def test_ragged_backtrack_matches_reference(device):
-    Q = 4
+@pytest.mark.parametrize("Q", [4, 20, 61])
+def test_ragged_backtrack_matches_reference(device, Q):
     chs, leaves = _batch(Q, seed=60)
     plan = RaggedTreePlan(chs, [L for _, L in SIZES])
     eng = RaggedSankoffEngine(plan, Q, device)
@@ -145,8 +148,8 @@ def test_from_padded_strips_trex_padding(device):
     assert shapes == [(2 * nl - 1, L) for nl, L in trees]
 
 
-def test_ragged_rejects_wide_q(device):
+def test_ragged_rejects_q_above_64(device):
     chs, _ = _batch(4, seed=1)
     plan = RaggedTreePlan(chs, [L for _, L in SIZES])
     with pytest.raises(NotImplementedError):
-        RaggedSankoffEngine(plan, 20, device)
+        RaggedSankoffEngine(plan, 65, device)

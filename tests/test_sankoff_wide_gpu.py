@@ -5,7 +5,9 @@ states bit-exact, hard gradient rtol 1e-6, softmin score / gradient /
 marginals rtol 1e-5 vs the fp64 oracle.  Q > 4 tables are site-major
 ([B][n_int][L][Q], trex_hip.h), so oracle tables are transposed to compare.
 Q = 20 is the protein alphabet of BASELINE config C3; 5, 13, 21 and 32
-exercise the padded-state groups (G = 8, 16, 32).
+exercise the padded-state groups (G = 8, 16, 32); 61 and 64 are codon
+alphabets (G = 64, one site per wave; trex sizes everything from n_states
+with no cap, sankoff.py:151-152).
 """
 
 from __future__ import annotations
@@ -56,7 +58,7 @@ def test_site_major_layout_flag(device):
     assert eng4.site_major and eng4.dp_shape == (1, 3, 10, 4)  # every Q since v4
 
 
-@pytest.mark.parametrize("Q", [5, 20, 21])
+@pytest.mark.parametrize("Q", [5, 20, 21, 61, 64])
 @pytest.mark.parametrize("L", [1, 7, 130, 1000])
 def test_run_sankoff_bitexact_wide(device, Q, L):
     ch = random_topologies(1, 16, seed=200 + L + Q)[0]
@@ -72,7 +74,8 @@ def test_run_sankoff_bitexact_wide(device, Q, L):
 
 
 @pytest.mark.parametrize("L,Q,n", [(1, 20, 8), (300, 20, 16), (1000, 20, 64), (777, 5, 12),
-                                   (513, 13, 20), (200, 32, 10), (64, 21, 9)])
+                                   (513, 13, 20), (200, 32, 10), (64, 21, 9), (300, 61, 12),
+                                   (65, 64, 9)])
 def test_batched_hard_fwd_grad_wide(device, L, Q, n):
     B = 4
     ch = random_topologies(B, n, seed=L + n + Q)
@@ -94,7 +97,7 @@ def test_batched_hard_fwd_grad_wide(device, L, Q, n):
     np.testing.assert_allclose(_sm(mg), ref["marginals"], rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("Q", [20, 7])
+@pytest.mark.parametrize("Q", [20, 7, 61])
 def test_backtrack_wide_matches_reference(device, Q):
     B, n, L = 3, 24, 515
     ch = random_topologies(B, n, seed=3 + Q)
@@ -113,7 +116,8 @@ def test_backtrack_wide_matches_reference(device, Q):
 
 
 @pytest.mark.parametrize("tau", [1.0, 0.5, 0.1])
-@pytest.mark.parametrize("L,n,Q", [(100, 8, 20), (1000, 64, 20), (301, 16, 6), (257, 12, 32)])
+@pytest.mark.parametrize("L,n,Q", [(100, 8, 20), (1000, 64, 20), (301, 16, 6), (257, 12, 32),
+                                   (129, 10, 61)])
 def test_softmin_fwd_grad_wide_vs_fp64(device, tau, L, n, Q):
     B = 2
     ch = random_topologies(B, n, seed=n + 13)

@@ -492,7 +492,6 @@ struct KArgs {
 // ragged plan per-tree record (ints): steps offset (in steps), n_int, n_leaves,
 // L, first site (site_score offset), first work item, leaf byte offset (lo, hi),
 // row-site offset of the tree's DP rows (lo, hi; x Q floats), 2 spare
-constexpr int kRaggedMeta = 12;
 
 
 // LDS map (floats): [0, 64) leaf tables: T[code][i] (message; code Q =
@@ -1552,6 +1551,7 @@ extern "C" int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int
 // ---------------------------------------------------------------------------
 extern "C" int64_t trex_ragged_workspace_bytes(int64_t items, int Q) {
   if (items <= 0 || Q <= 0) return 0;
+  if (Q > 4) return wide_ragged_workspace_bytes(items, Q);  // partials per wave
   return items * 8 * (1 + (int64_t)Q * Q) + 256;
 }
 
@@ -1566,7 +1566,9 @@ extern "C" int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_
   if (B <= 0 || items <= 0 || items > 0x7FFFFFFF || max_nl < 2 || Q < 2)
     return set_error(TREX_E_ARG, "%s: bad shape B=%d items=%lld max_nl=%d Q=%d", fn, B,
                      (long long)items, max_nl, Q);
-  if (Q > 4) return set_error(TREX_E_UNSUPPORTED, "%s: ragged batches support Q <= 4", fn);
+  if (Q > kWideMaxQ)
+    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build", fn, Q,
+                     kWideMaxQ);
   if (!plan || !leaves || !cost || !workspace || !dp)
     return set_error(TREX_E_ARG, "%s: null pointer argument", fn);
   if ((phase & 1) && !tree_score) return set_error(TREX_E_ARG, "%s: tree_score is required", fn);
@@ -1576,6 +1578,35 @@ extern "C" int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_
   if (workspace_bytes < trex_ragged_workspace_bytes(items, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
   if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  if (Q > 4) {
+    // protein / codon alphabets: the state-parallel kernel, each 64-site
+    // item split over ceil(64 / sites-per-wave) waves
+    const int* meta = plan + TREX_PLAN_HEADER_INTS;
+    WideCall c;
+    c.phase = phase;
+    c.soft = tau > 0.0f;
+    c.steps = meta + (size_t)B * kRaggedMeta + items;
+    c.leaves = leaves;
+    c.cost = cost;
+    c.B = B;
+    c.L = 0;
+    c.nl = max_nl;
+    c.ni = max_nl - 1;
+    c.Q = Q;
+    c.n_slots = n_slots;
+    tau_coefs(tau, &c.a, &c.bcoef);
+    c.hard_root = (flags & TREX_FLAG_HARD_ROOT) ? 1 : 0;
+    c.dp = dp;
+    c.site_score = site_score;
+    c.tree_score = tree_score;
+    c.dts = d_tree_score;
+    c.marg = marginals;
+    c.anc = anc_states;
+    c.d_cost = d_cost;
+    c.workspace = workspace;
+    c.stream = stream;
+    return wide_ragged_run(fn, c, meta, meta + (size_t)B * kRaggedMeta, items);
+  }
   const size_t lds = lds_bytes(n_slots, max_nl, Q, 1);
   if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
   KArgs A;
@@ -1622,13 +1653,16 @@ extern "C" int trex_sankoff_ragged_backtrack(const int32_t* plan, int B, int64_t
   const char* fn = "trex_sankoff_ragged_backtrack";
   if (B <= 0 || items <= 0 || items > 0x7FFFFFFF || steps <= 0 || Q < 2)
     return set_error(TREX_E_ARG, "%s: bad arguments", fn);
-  if (Q > 4) return set_error(TREX_E_UNSUPPORTED, "%s: ragged batches support Q <= 4", fn);
+  if (Q > kWideMaxQ)
+    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build", fn, Q,
+                     kWideMaxQ);
   if (!backtrack_ok)
     return set_error(TREX_E_TOPOLOGY,
                      "%s: the reference backtrack does not terminate on this batch (cyclic child "
                      "references)", fn);
   if (!plan || !cost || !dp || !anc_states) return set_error(TREX_E_ARG, "%s: null pointer", fn);
   const int* meta = plan + TREX_PLAN_HEADER_INTS;
+  if (Q > 4) return wide_ragged_backtrack(meta, B, items, steps, cost, dp, Q, anc_states, stream);
   hipStream_t st = (hipStream_t)stream;
 #define TREX_RBT(QQ)                                                                          \
   hipLaunchKernelGGL((sankoff_backtrack_kernel<QQ, 1, true>), dim3((int)items), dim3(kWave), 0, \

@@ -588,6 +588,7 @@ extern "C" int trex_debug_stage_rt(unsigned long long* out) {
 #endif
 
 size_t staged_lds_bytes(int ni, int nl, int Q, int phase) {
+  if (Q > 32) return ~(size_t)0;  // codons: one site per wave already, wide kernel
   switch (wide_group(Q)) {
     case 4: return staged_lds_g<4>(ni, nl, Q, phase);
     case 8: return staged_lds_g<8>(ni, nl, Q, phase);
@@ -598,6 +599,7 @@ size_t staged_lds_bytes(int ni, int nl, int Q, int phase) {
 }
 
 int staged_run(const char* fn, const WideCall& c, const int32_t* staged) {
+  if (c.Q > 32) return set_error(TREX_E_UNSUPPORTED, "%s: staged kernel needs Q <= 32", fn);
   const int tiles = wide_tiles(c.L, c.Q);
   const size_t lds = staged_lds_bytes(c.ni, c.nl, c.Q, c.phase);
   if (lds > 160 * 1024) return set_error(TREX_E_UNSUPPORTED, "%s: staged LDS too large", fn);

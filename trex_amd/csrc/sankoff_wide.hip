@@ -43,8 +43,13 @@ struct WArgs {
   const float* dts;   // [B] or null
   float* marg;        // [B][n_int][L][Q] or null
   int8_t* anc;        // [B][n_int][L] or null
-  double* part_tree;  // [B * tiles]
-  double* part_dc;    // [Q * Q][B * tiles]
+  double* part_tree;  // [B * tiles] (ragged: [items * wpi])
+  double* part_dc;    // [Q * Q][grid]
+  // ragged batches (plan.cpp trex_ragged_plan_build): per-tree records and
+  // the 64-site work item -> tree table; wpi waves per item (SPW sites each)
+  const int* rmeta;
+  const int* ritem;
+  int wpi;
 };
 
 // LDS map (floats): 4 exchange buffers [4][64], leaf message table
@@ -52,15 +57,13 @@ struct WArgs {
 // slots [n_slots + 1][64] (n_slots = root cotangent), leaf tile [nl][64/G] i8
 // (exchange helpers, wmsg / wadj: wide_dev.h)
 
-template <int G, int MODE, int PHASE, bool LFAST, bool SYM>
+template <int G, int MODE, int PHASE, bool LFAST, bool SYM, bool RAGGED>
 __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in, float* lds) {
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
   constexpr int SPW = kWave / G;
   const int Q = A.Q;
-  const int tree = blockIdx.x / A.tiles;
-  const int tile = blockIdx.x - tree * A.tiles;
   const int lane = threadIdx.x;
   const int grp = lane / G;
   WLane w;
@@ -68,9 +71,40 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
   w.i = lane - grp * G;
   w.gbase = (grp < SPW ? grp : 0) * G;
   w.pad = w.i >= Q;
-  const int site = tile * SPW + grp;
-  const bool active = grp < SPW && site < A.L;
-  const int L = A.L;
+  // this wave's tree, shape and site groups: uniform batches tile each tree
+  // in SPW-site items; ragged batches split each 64-site item of the plan
+  // into wpi waves of SPW sites
+  int tree, n_int, nl, L, site0;
+  size_t leaf_base, rows_base, site_base;
+  const int* steps;
+  int in_item = SPW;  // groups of this wave inside the item
+  if constexpr (RAGGED) {
+    const int item = blockIdx.x / A.wpi;
+    const int sub = blockIdx.x - item * A.wpi;
+    tree = as_const(A.ritem)[item];
+    const cptr<int> m = as_const(A.rmeta) + (size_t)tree * kRaggedMeta;
+    n_int = m[1];
+    nl = m[2];
+    L = m[3];
+    site_base = (size_t)(uint32_t)m[4];
+    site0 = (item - m[5]) * kWave + sub * SPW;
+    in_item = kWave - sub * SPW;
+    leaf_base = (size_t)(uint32_t)m[6] | ((size_t)(uint32_t)m[7] << 32);
+    rows_base = (size_t)(uint32_t)m[8] | ((size_t)(uint32_t)m[9] << 32);
+    steps = A.steps + (size_t)m[0] * 4;
+  } else {
+    tree = blockIdx.x / A.tiles;
+    n_int = A.n_int;
+    nl = A.nl;
+    L = A.L;
+    site0 = (blockIdx.x - tree * A.tiles) * SPW;
+    leaf_base = (size_t)tree * nl * L;
+    rows_base = (size_t)tree * n_int * L;
+    site_base = (size_t)tree * L;
+    steps = A.steps + (size_t)tree * n_int * 4;
+  }
+  const int site = site0 + grp;
+  const bool active = grp < SPW && grp < in_item && site < L;
   const float a = A.a, bcoef = A.bcoef;
 
   float* X = lds;
@@ -88,7 +122,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
   constexpr bool KEEP_MD = PHASE == 3 && MODE == kSoftK && G > 4;
 #endif
   float* mdc = slots + (A.n_slots + 1) * kWave;
-  int8_t* lleaf = reinterpret_cast<int8_t*>(mdc + (size_t)A.n_int * SPW);
+  int8_t* lleaf = reinterpret_cast<int8_t*>(mdc + (size_t)(A.nl - 1) * SPW);  // A.nl: max leaves
 
   // ---- prologue: leaf tables + leaf tile ----
   {
@@ -102,21 +136,22 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
       tab[Q * G + w.i] = sent;
       if constexpr (!SYM) fill_col_table<G, MODE>(ctab, A.cost, Q, w.i, cf.cmin, a);
     }
-    const int8_t* lv = A.leaves + (size_t)tree * A.nl * L;
-    for (int t = lane; t < A.nl * SPW; t += kWave) {
+    const int8_t* lv = A.leaves + leaf_base;
+    for (int t = lane; t < nl * SPW; t += kWave) {
       const int leaf = t / SPW;
-      const int s = tile * SPW + (t - leaf * SPW);
-      int code = s < L ? (int)lv[(size_t)leaf * L + s] : Q;
+      const int g = t - leaf * SPW;
+      const int s = site0 + g;
+      int code = (g < in_item && s < L) ? (int)lv[(size_t)leaf * L + s] : Q;
       code = ((unsigned)code < (unsigned)Q) ? code : Q;
       lleaf[t] = (int8_t)code;
     }
     wave_sync();
   }
 
-  const cptr<int> prog = as_const(A.steps) + (size_t)tree * A.n_int * 4;
+  const cptr<int> prog = as_const(steps);
   const uint32_t rowbytes = (uint32_t)L * Q * 4;
-  const uint32_t treebytes = (uint32_t)A.n_int * rowbytes;
-  const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * A.n_int * L * Q, treebytes);
+  const uint32_t treebytes = (uint32_t)n_int * rowbytes;
+  const rsrc_t rdp = make_rsrc(A.dp + rows_base * Q, treebytes);
   // inactive sites and padded states address past the buffer: stores drop, loads give 0
   const int voff = (active && !w.pad) ? (site * Q + w.i) * 4 : 0x7FFFFFF0;
   const int lgrp = grp < SPW ? grp : 0;
@@ -125,9 +160,9 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
   if constexpr (FWD) {
     float prev = 0.0f;  // previous step's D (register bypass, kChildPrev)
     I4 nxt = load_step(prog, 0);
-    for (int k = 0; k < A.n_int; ++k) {
+    for (int k = 0; k < n_int; ++k) {
       const I4 stp = nxt;
-      if (k + 1 < A.n_int) nxt = load_step(prog, k + 1);
+      if (k + 1 < n_int) nxt = load_step(prog, k + 1);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int desc = c == 0 ? stp.y : stp.z;
@@ -162,7 +197,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
     }
   } else {
     dv = __uint_as_float(
-        __builtin_amdgcn_raw_buffer_load_b32(rdp, voff, (A.n_int - 1) * rowbytes, 0));
+        __builtin_amdgcn_raw_buffer_load_b32(rdp, voff, (n_int - 1) * rowbytes, 0));
   }
 
   // ---- root: score + cotangent (sankoff.py:187) ----
@@ -192,7 +227,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
   }
   const bool leader = active && w.i == 0;
   if constexpr (FWD) {
-    if (leader && A.site_score) A.site_score[(size_t)tree * L + site] = score;
+    if (leader && A.site_score) A.site_score[site_base + site] = score;
     const double tot = wave_sum(leader ? (double)score : 0.0);
     if (lane == 0) A.part_tree[blockIdx.x] = tot;
   }
@@ -204,14 +239,13 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
     const float dscale = A.dts ? as_const(A.dts)[tree] : 1.0f;
     slots[A.n_slots * kWave + lane] = active ? groot * dscale : 0.0f;
     const bool want_marg = A.marg != nullptr;
-    const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * A.n_int * L * Q : A.dp,
-                                 treebytes);
+    const rsrc_t rmg = make_rsrc(want_marg ? A.marg + rows_base * Q : A.dp, treebytes);
     const bool want_anc = A.anc != nullptr;
-    int8_t* at = want_anc ? A.anc + (size_t)tree * A.n_int * L + site : nullptr;
+    int8_t* at = want_anc ? A.anc + rows_base + site : nullptr;
 
     // the next step's internal-child DP values are loaded one step ahead
     float nd[2] = {0.0f, 0.0f};
-    I4 nstp = load_step(prog, A.n_int - 1);
+    I4 nstp = load_step(prog, n_int - 1);
     auto prefetch = [&](const I4& s2) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -223,7 +257,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
     };
     prefetch(nstp);
     float gnext = 0.0f;  // cotangent handed to the next reverse step (bypass)
-    for (int k = A.n_int - 1; k >= 0; --k) {
+    for (int k = n_int - 1; k >= 0; --k) {
       const I4 stp = nstp;
       const float cd0 = nd[0], cd1 = nd[1];
       if (k > 0) {
@@ -280,7 +314,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
     }
 
     // ---- per-wave dC partial: rows i summed over the wave's sites ----
-    const int nb = A.B * A.tiles;
+    const int nb = gridDim.x;
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       double v = (double)acc[j];
@@ -294,15 +328,15 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
   }
 }
 
-template <int G, int MODE, int PHASE, bool SYM = false>
+template <int G, int MODE, int PHASE, bool RAGGED, bool SYM = false>
 __device__ __forceinline__ void wide_dispatch_leaf(const WArgs& A, const WCoef<G>& cf, float cmax,
                                                    float* lds) {
   const float range = cmax - cf.cmin;
   const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
   if (lfast)
-    wide_body<G, MODE, PHASE, true, SYM>(A, cf, lds);
+    wide_body<G, MODE, PHASE, true, SYM, RAGGED>(A, cf, lds);
   else
-    wide_body<G, MODE, PHASE, false, SYM>(A, cf, lds);
+    wide_body<G, MODE, PHASE, false, SYM, RAGGED>(A, cf, lds);
 }
 
 #ifndef TREX_WIDE_MINW
@@ -313,7 +347,7 @@ __device__ __forceinline__ void wide_dispatch_leaf(const WArgs& A, const WCoef<G
 template <int G, int PHASE>
 constexpr int wide_min_blocks() { return (G == 20 && (PHASE & 2)) ? TREX_WIDE_MINW : 1; }
 
-template <int G, bool SOFT, int PHASE>
+template <int G, bool SOFT, int PHASE, bool RAGGED = false>
 __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_wide_kernel(WArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int Q = A.Q;
@@ -322,19 +356,20 @@ __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_
   bool sym;
   cost_range<G>(A.cost, Q, i, cmin, cmax, &sym);
   if constexpr (!SOFT) {
-    wide_dispatch_leaf<G, kHard, PHASE>(A, make_coefs<G, kHard>(A.cost, Q, i, cmin, A.a), cmax, lds);
+    wide_dispatch_leaf<G, kHard, PHASE, RAGGED>(A, make_coefs<G, kHard>(A.cost, Q, i, cmin, A.a), cmax,
+                                                lds);
   } else if (use_ktrick(cmin, cmax, A.a)) {
     // symmetric costs (C3's protein matrix; C = 1 - I): K's column i is row
     // i, a variant without the column registers
     if (G > 4 && sym)
-      wide_dispatch_leaf<G, kSoftK, PHASE, G != 4>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a),
-                                                   cmax, lds);
+      wide_dispatch_leaf<G, kSoftK, PHASE, RAGGED, G != 4>(
+          A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a), cmax, lds);
     else
-      wide_dispatch_leaf<G, kSoftK, PHASE>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a), cmax,
-                                           lds);
+      wide_dispatch_leaf<G, kSoftK, PHASE, RAGGED>(A, make_coefs<G, kSoftK>(A.cost, Q, i, cmin, A.a),
+                                                   cmax, lds);
   } else {
-    wide_dispatch_leaf<G, kSoftDirect, PHASE>(A, make_coefs<G, kSoftDirect>(A.cost, Q, i, cmin, A.a),
-                                              cmax, lds);
+    wide_dispatch_leaf<G, kSoftDirect, PHASE, RAGGED>(
+        A, make_coefs<G, kSoftDirect>(A.cost, Q, i, cmin, A.a), cmax, lds);
   }
 }
 
@@ -347,7 +382,8 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
                                                           float* __restrict__ tree_score,
                                                           float* __restrict__ d_cost,
                                                           const int* __restrict__ first,
-                                                          int first_stride, int items) {
+                                                          int first_stride, int items,
+                                                          int first_scale) {
   __shared__ double red[256];
   const int b = blockIdx.x;
   const double* src;
@@ -355,8 +391,8 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
   float* dst;
   if (do_tree && b < B) {
     if (first) {  // ragged: tree b owns items [first[b], first[b + 1])
-      const int lo = first[(size_t)b * first_stride];
-      const int hi = b + 1 < B ? first[(size_t)(b + 1) * first_stride] : items;
+      const int lo = first[(size_t)b * first_stride] * first_scale;
+      const int hi = (b + 1 < B ? first[(size_t)(b + 1) * first_stride] : items) * first_scale;
       src = part_tree + lo;
       n = hi - lo;
     } else {
@@ -366,7 +402,7 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
     dst = tree_score + b;
   } else {
     const int q = b - (do_tree ? B : 0);
-    const size_t nb = first ? (size_t)items : (size_t)B * tiles;
+    const size_t nb = first ? (size_t)items * first_scale : (size_t)B * tiles;
     src = part_dc + (size_t)q * nb;
     n = (int)nb;
     dst = d_cost + q;
@@ -384,33 +420,52 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
 // states written so far stay in LDS ([n_int][64] bytes per wave) for the
 // children's parent lookups instead of a global store -> load round trip
 // on the chain.
+template <int MQ, bool RAGGED = false>  // MQ 32: Q <= 32; 64: codon alphabets
 __global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __restrict__ bt,
                                                                const float* __restrict__ cost,
                                                                const float* __restrict__ dp,
                                                                int n_int, int L, int Q, int tiles,
-                                                               int8_t* __restrict__ anc) {
+                                                               int8_t* __restrict__ anc,
+                                                               const int* __restrict__ rmeta = nullptr,
+                                                               int B = 0, int items = 0,
+                                                               int steps = 0) {
   extern __shared__ __attribute__((aligned(16))) float bl[];
-  float* c = bl;                                              // [32][32]
-  int8_t* sts = reinterpret_cast<int8_t*>(bl + 32 * 32);      // [n_int][64]
-  const int tree = blockIdx.x / tiles;
-  const int tile = blockIdx.x - tree * tiles;
+  float* c = bl;                                                // [Q][Q]
+  int8_t* sts = reinterpret_cast<int8_t*>(bl + MQ * MQ);        // [n_int][64]
+  int tree, tile;
+  size_t rows_base;
+  if constexpr (RAGGED) {  // ragged plan: per-tree record, item table, steps, entries
+    const int item = blockIdx.x;
+    tree = as_const(rmeta + (size_t)B * kRaggedMeta)[item];
+    const cptr<int> m = as_const(rmeta) + (size_t)tree * kRaggedMeta;
+    n_int = m[1];
+    L = m[3];
+    tile = item - m[5];
+    rows_base = (size_t)(uint32_t)m[8] | ((size_t)(uint32_t)m[9] << 32);
+    bt = rmeta + (size_t)B * kRaggedMeta + items + (size_t)steps * 4 + (size_t)m[0] * 2;
+  } else {
+    tree = blockIdx.x / tiles;
+    tile = blockIdx.x - tree * tiles;
+    rows_base = (size_t)tree * n_int * L;
+    bt += (size_t)tree * n_int * 2;
+  }
   const int lane = threadIdx.x;
   for (int t = lane; t < Q * Q; t += kWave) c[t] = cost[t];
   __syncthreads();
   const int site = tile * kWave + lane;
   if (site >= L) return;
-  const cptr<int> prog = as_const(bt) + (size_t)tree * n_int * 2;
-  const float* dpt = dp + (size_t)tree * n_int * L * Q + (size_t)site * Q;
-  int8_t* at = anc + (size_t)tree * n_int * L + site;
+  const cptr<int> prog = as_const(bt);
+  const float* dpt = dp + rows_base * Q + (size_t)site * Q;
+  int8_t* at = anc + rows_base + site;
   // rows are 16-B aligned when Q % 4 == 0 (site * Q * 4): dwordx4 loads, a
   // quarter of the address work of 4-byte loads at an 4Q-byte lane stride
   const bool vec = (Q & 3) == 0;
-  auto load_row = [&](int k, float (&o)[32]) {
+  auto load_row = [&](int k, float (&o)[MQ]) {
     const int x = (k < n_int) ? (prog[2 * k] & 0xFFFF) : 0;
     const float* d = dpt + (size_t)x * L * Q;
     if (vec) {
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
+      for (int v = 0; v < MQ / 4; ++v) {
         const float4 w = (4 * v < Q) ? reinterpret_cast<const float4*>(d)[v]
                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         o[4 * v] = w.x;
@@ -420,10 +475,10 @@ __global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __rest
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 32; ++j) o[j] = (j < Q) ? d[j] : 0.0f;
+      for (int j = 0; j < MQ; ++j) o[j] = (j < Q) ? d[j] : 0.0f;
     }
   };
-  auto step = [&](int k, const float (&d)[32]) {
+  auto step = [&](int k, const float (&d)[MQ]) {
     const int ex = prog[2 * k], ey = prog[2 * k + 1];
     const int x = ex & 0xFFFF;
     const int kind = (ex >> 16) & 0xF;
@@ -433,27 +488,29 @@ __global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __rest
       if (kind == kBtRoot) {
         float bv = d[0];
 #pragma unroll
-        for (int j = 1; j < 32; ++j) {
+        for (int j = 1; j < MQ; ++j) {
           if (j >= Q) break;
           const float v = d[j];
           if (v < bv) { bv = v; out = j; }
         }
       } else {
-        const int sp = sts[ey * kWave + lane];
+        // parent's state: LDS for uniform batches; ragged batches (no bound
+        // on a tree's node count at launch) re-read this lane's own output
+        const int sp = RAGGED ? (int)at[(size_t)ey * L] : (int)sts[ey * kWave + lane];
         const float* row = c + sp * Q;
         float bv = row[0] + (sent ? kSentinel : d[0]);
 #pragma unroll
-        for (int j = 1; j < 32; ++j) {
+        for (int j = 1; j < MQ; ++j) {
           if (j >= Q) break;
           const float v = row[j] + (sent ? kSentinel : d[j]);
           if (v < bv) { bv = v; out = j; }
         }
       }
     }
-    sts[x * kWave + lane] = (int8_t)out;
+    if constexpr (!RAGGED) sts[x * kWave + lane] = (int8_t)out;
     at[(size_t)x * L] = (int8_t)out;
   };
-  float r0[32], r1[32];
+  float r0[MQ], r1[MQ];
   load_row(0, r0);
   for (int k = 0; k < n_int; k += 2) {
     load_row(k + 1, r1);
@@ -464,22 +521,22 @@ __global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __rest
   }
 }
 
-template <int G, bool SOFT>
+template <int G, bool SOFT, bool RAGGED>
 void launch_wide(int phase, int grid, size_t lds, hipStream_t st, const WArgs& A) {
   if (phase == 1)
-    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 1>), dim3(grid), dim3(kWave), lds, st, A);
+    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 1, RAGGED>), dim3(grid), dim3(kWave), lds, st, A);
   else if (phase == 2)
-    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 2>), dim3(grid), dim3(kWave), lds, st, A);
+    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 2, RAGGED>), dim3(grid), dim3(kWave), lds, st, A);
   else
-    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 3>), dim3(grid), dim3(kWave), lds, st, A);
+    hipLaunchKernelGGL((sankoff_wide_kernel<G, SOFT, 3, RAGGED>), dim3(grid), dim3(kWave), lds, st, A);
 }
 
-template <int G>
+template <int G, bool RAGGED = false>
 void launch_wide_g(int phase, bool soft, int grid, size_t lds, hipStream_t st, const WArgs& A) {
   if (soft)
-    launch_wide<G, true>(phase, grid, lds, st, A);
+    launch_wide<G, true, RAGGED>(phase, grid, lds, st, A);
   else
-    launch_wide<G, false>(phase, grid, lds, st, A);
+    launch_wide<G, false, RAGGED>(phase, grid, lds, st, A);
 }
 
 }  // namespace
@@ -489,7 +546,8 @@ int wide_group(int Q) {
   if (Q <= 8) return 8;
   if (Q <= 16) return 16;
   if (Q <= 20) return 20;
-  return 32;
+  if (Q <= 32) return 32;
+  return 64;  // codon alphabets (61 / 64): one site per wave
 }
 
 int wide_tiles(int L, int Q) {
@@ -536,6 +594,9 @@ int wide_run(const char* fn, const WideCall& c) {
   A.dts = c.dts;
   A.marg = c.marg;
   A.anc = c.anc;
+  A.rmeta = nullptr;
+  A.ritem = nullptr;
+  A.wpi = 0;
   const int64_t nb = (int64_t)c.B * tiles;
   A.part_tree = static_cast<double*>(c.workspace);
   A.part_dc = A.part_tree + nb;
@@ -546,7 +607,8 @@ int wide_run(const char* fn, const WideCall& c) {
     case 8: launch_wide_g<8>(c.phase, c.soft, grid, lds, st, A); break;
     case 16: launch_wide_g<16>(c.phase, c.soft, grid, lds, st, A); break;
     case 20: launch_wide_g<20>(c.phase, c.soft, grid, lds, st, A); break;
-    default: launch_wide_g<32>(c.phase, c.soft, grid, lds, st, A); break;
+    case 32: launch_wide_g<32>(c.phase, c.soft, grid, lds, st, A); break;
+    default: launch_wide_g<64>(c.phase, c.soft, grid, lds, st, A); break;
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
@@ -554,31 +616,111 @@ int wide_run(const char* fn, const WideCall& c) {
                         c.d_cost, c.stream);
 }
 
+// waves per 64-site ragged item: ceil(64 / sites per wave)
+int wide_ragged_wpi(int Q) {
+  const int spw = kWave / wide_group(Q);
+  return (kWave + spw - 1) / spw;
+}
+
+int64_t wide_ragged_workspace_bytes(int64_t items, int Q) {
+  return items * wide_ragged_wpi(Q) * 8 * (1 + (int64_t)Q * Q) + 256;
+}
+
+int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const int* ritem,
+                    int64_t items) {
+  const int wpi = wide_ragged_wpi(c.Q);
+  const size_t lds = wide_lds_bytes(c.n_slots, c.nl, c.nl - 1, c.Q);
+  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
+  if (items * wpi > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
+  WArgs A;
+  A.steps = c.steps;
+  A.leaves = c.leaves;
+  A.cost = c.cost;
+  A.n_int = 0;
+  A.nl = c.nl;  // max leaves (LDS leaf tile, stabiliser rows)
+  A.L = 0;
+  A.tiles = 0;
+  A.B = c.B;
+  A.n_slots = c.n_slots;
+  A.Q = c.Q;
+  A.a = c.a;
+  A.bcoef = c.bcoef;
+  A.hard_root = c.hard_root;
+  A.dp = c.dp;
+  A.site_score = c.site_score;
+  A.dts = c.dts;
+  A.marg = c.marg;
+  A.anc = c.anc;
+  A.rmeta = rmeta;
+  A.ritem = ritem;
+  A.wpi = wpi;
+  const int grid = (int)(items * wpi);
+  A.part_tree = static_cast<double*>(c.workspace);
+  A.part_dc = A.part_tree + grid;
+  hipStream_t st = (hipStream_t)c.stream;
+  switch (wide_group(c.Q)) {
+    case 8: launch_wide_g<8, true>(c.phase, c.soft, grid, lds, st, A); break;
+    case 16: launch_wide_g<16, true>(c.phase, c.soft, grid, lds, st, A); break;
+    case 20: launch_wide_g<20, true>(c.phase, c.soft, grid, lds, st, A); break;
+    case 32: launch_wide_g<32, true>(c.phase, c.soft, grid, lds, st, A); break;
+    default: launch_wide_g<64, true>(c.phase, c.soft, grid, lds, st, A); break;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return partial_reduce(fn, A.part_tree, A.part_dc, c.B, 0, c.Q, c.phase, c.tree_score, c.d_cost,
+                        c.stream, rmeta + 5, kRaggedMeta, (int)items, wpi);
+}
+
 int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
                    int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream,
-                   const int* first, int first_stride, int items) {
+                   const int* first, int first_stride, int items, int first_scale) {
   const bool do_tree = (phase & 1) != 0;
   const bool do_dc = (phase & 2) != 0;
   const int rgrid = (do_tree ? B : 0) + (do_dc ? Q * Q : 0);
   hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(256), 0, (hipStream_t)stream,
                      part_tree, part_dc, B, tiles, Q * Q, do_tree ? 1 : 0, tree_score, d_cost,
-                     first, first_stride, items);
+                     first, first_stride, items, first_scale);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return TREX_OK;
+}
+
+int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,
+                          const float* cost, const float* dp, int Q, int8_t* anc, void* stream) {
+  const int mq = Q <= 32 ? 32 : 64;
+  const size_t lds = (size_t)mq * mq * 4;
+  if (mq == 32)
+    hipLaunchKernelGGL((wide_backtrack_kernel<32, true>), dim3((int)items), dim3(kWave), lds,
+                       (hipStream_t)stream, nullptr, cost, dp, 0, 0, Q, 0, anc, rmeta, B,
+                       (int)items, (int)steps);
+  else
+    hipLaunchKernelGGL((wide_backtrack_kernel<64, true>), dim3((int)items), dim3(kWave), lds,
+                       (hipStream_t)stream, nullptr, cost, dp, 0, 0, Q, 0, anc, rmeta, B,
+                       (int)items, (int)steps);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return set_error(TREX_E_HIP, "trex_sankoff_ragged_backtrack: %s", hipGetErrorString(e));
   return TREX_OK;
 }
 
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream) {
   const int tiles = (L + kWave - 1) / kWave;
-  const size_t lds = 32 * 32 * 4 + (size_t)ni * kWave;
+  const int mq = Q <= 32 ? 32 : 64;
+  const size_t lds = (size_t)mq * mq * 4 + (size_t)ni * kWave;
   if (lds > 160 * 1024)
     return set_error(TREX_E_UNSUPPORTED, "trex_sankoff_backtrack: %d internal nodes", ni);
-  if (lds > 65536)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(wide_backtrack_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(wide_backtrack_kernel, dim3(B * tiles), dim3(kWave), lds, (hipStream_t)stream,
-                     bt, cost, dp, ni, L, Q, tiles, anc);
+  auto go = [&](auto kernel) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kernel, dim3(B * tiles), dim3(kWave), lds, (hipStream_t)stream, bt, cost, dp,
+                       ni, L, Q, tiles, anc, (const int*)nullptr, 0, 0, 0);
+  };
+  if (mq == 32)
+    go(wide_backtrack_kernel<32, false>);
+  else
+    go(wide_backtrack_kernel<64, false>);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)
     return set_error(TREX_E_HIP, "trex_sankoff_backtrack: %s", hipGetErrorString(e));

@@ -84,7 +84,8 @@ struct WideCall {
   void* workspace;
   void* stream;
 };
-constexpr int kWideMaxQ = 32;
+constexpr int kWideMaxQ = 64;
+constexpr int kRaggedMeta = 12;  // ints per tree record of a ragged plan (plan.cpp)  // leaf codes and ancestral states are int8
 int wide_group(int Q);
 int wide_tiles(int L, int Q);
 size_t wide_lds_bytes(int n_slots, int nl, int ni, int Q);
@@ -98,10 +99,19 @@ int staged_run(const char* fn, const WideCall& c, const int32_t* staged);
 // [Q*Q] (phase & 2); part_dc is [Q*Q][B*tiles]
 // (ragged batches: first[b * first_stride] is tree b's first item, items the
 // total; tiles is then unused)
+// (first_scale: partials per item, the wide kernel's waves per ragged item)
 int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
                    int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream,
-                   const int* first = nullptr, int first_stride = 0, int items = 0);
+                   const int* first = nullptr, int first_stride = 0, int items = 0,
+                   int first_scale = 1);
+// ragged batches with Q > 4 on the wide kernel (rmeta / ritem: the plan's
+// records and item table; c.nl = max leaves, c.L unused)
+int64_t wide_ragged_workspace_bytes(int64_t items, int Q);
+int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const int* ritem,
+                    int64_t items);
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream);
+int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,
+                          const float* cost, const float* dp, int Q, int8_t* anc, void* stream);
 
 }  // namespace trex

@@ -104,7 +104,8 @@ class RaggedTreePlan:
 
 
 class RaggedSankoffEngine:
-    """Sankoff over a ragged batch on the device (Q <= 4).
+    """Sankoff over a ragged batch on the device (Q <= 64: Q <= 4 lane per
+    site, larger alphabets state-parallel, sankoff_wide.hip).
 
     leaves: packed int8 device tensor (RaggedTreePlan.pack_leaves); cost (Q, Q)
     float32.  Mirrors SankoffEngine's forward / backward / fwd_bwd /
@@ -113,8 +114,8 @@ class RaggedSankoffEngine:
 
     def __init__(self, plan: RaggedTreePlan, n_states: int, device=None):
         torch = _torch()
-        if n_states > 4:
-            raise NotImplementedError("ragged batches support Q <= 4")
+        if n_states > 64:
+            raise NotImplementedError("alphabets above 64 states are not supported")
         self.plan = plan
         self.Q = int(n_states)
         self.device = torch.device(device) if device is not None else torch.device(
