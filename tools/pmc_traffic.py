@@ -38,7 +38,7 @@ def main():
     ap.add_argument("pmc")
     ap.add_argument("calib")
     ap.add_argument("--out", default=None)
-    ap.add_argument("--workload-key", default="128x32x5000x4")
+    ap.add_argument("--workload-key", default="1024x32x5000x4")
     a = ap.parse_args()
     known = 128 * 31 * 4 * 5000 * 4  # bytes per calibration launch
     cal = {short(k): v for k, v in counters(a.calib).items()}

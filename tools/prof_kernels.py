@@ -1,4 +1,4 @@
-"""Run each Sankoff entry point ITERS times on the bench workload (C4 shard),
+"""Run each Sankoff entry point ITERS times on the bench workload (C4, 1024 trees),
 for rocprofv3 kernel-trace / PMC collection.
 
     rocprofv3 --kernel-trace --stats -d OUT -o run --output-format csv -- \
@@ -16,7 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="all")
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--trees", type=int, default=128)
+    ap.add_argument("--trees", type=int, default=1024)
     ap.add_argument("--taxa", type=int, default=32)
     ap.add_argument("--sites", type=int, default=5000)
     ap.add_argument("--tau", type=float, default=0.5)
@@ -27,7 +27,7 @@ def main():
     from trex_amd import SankoffEngine
 
     dev = torch.device("cuda", 0)
-    ch, plan, leaves, cost = make_inputs(torch, dev, a.trees, a.taxa, a.sites, 4, 0)
+    ch, plan, leaves, cost = make_inputs(torch, dev, a.trees, a.taxa, a.sites, 4, 0, a.trees)
     eng = SankoffEngine(plan, a.sites, 4, dev)
     st = Step(torch, eng, leaves, cost, a.tau)
     st.fwd()

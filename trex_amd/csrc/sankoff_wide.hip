@@ -376,7 +376,10 @@ __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_
 // fixed-order reduction of per-item partials (both Sankoff paths): blocks
 // [0, B) = tree scores, blocks [B, B + Q*Q) = dC entries; bitwise
 // reproducible, and no arrival counters, so launches replay in hipGraphs
-__global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restrict__ part_tree,
+// 1 024 threads per entry: C4's dC entries sum 80 896 item partials each
+// (28 -> ~8 us at 256 threads)
+constexpr int kReduceThreads = 1024;
+__global__ __launch_bounds__(kReduceThreads) void wide_reduce_kernel(const double* __restrict__ part_tree,
                                                           const double* __restrict__ part_dc,
                                                           int B, int tiles, int Q2, int do_tree,
                                                           float* __restrict__ tree_score,
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
                                                           const int* __restrict__ first,
                                                           int first_stride, int items,
                                                           int first_scale) {
-  __shared__ double red[256];
+  __shared__ double red[kReduceThreads];
   const int b = blockIdx.x;
   const double* src;
   int n;
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(256) void wide_reduce_kernel(const double* __restri
     n = (int)nb;
     dst = d_cost + q;
   }
-  const double v = fixed_sum256(src, n, red, threadIdx.x);
+  const double v = fixed_sum<kReduceThreads>(src, n, red, threadIdx.x);
   if (threadIdx.x == 0) *dst = (float)v;
 }
 
@@ -677,7 +680,7 @@ int partial_reduce(const char* fn, const double* part_tree, const double* part_d
   const bool do_tree = (phase & 1) != 0;
   const bool do_dc = (phase & 2) != 0;
   const int rgrid = (do_tree ? B : 0) + (do_dc ? Q * Q : 0);
-  hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(kReduceThreads), 0, (hipStream_t)stream,
                      part_tree, part_dc, B, tiles, Q * Q, do_tree ? 1 : 0, tree_score, d_cost,
                      first, first_stride, items, first_scale);
   const hipError_t e = hipGetLastError();

@@ -437,26 +437,22 @@ __device__ __forceinline__ float wadj_k_md(const WCoef<G>& cf, float* X, const W
   return u * kdot_col<G, SYM>(cf, rr);
 }
 
-// Fixed-order sum of n doubles by 256 threads (t = 0..255 of a group that
-// owns red[256]); the result is in thread 0's return value.  Eight
-// independent accumulators keep eight loads in flight per thread; the
-// association is fixed, so the reduce kernel and the staged kernel's
-// in-kernel tail give bitwise the same sums.  Every thread of the block
-// must call it (it contains __syncthreads()).  COHERENT: device-scope loads
-// (partials other workgroups wrote during the same launch).
-template <bool COHERENT = false>
-__device__ __forceinline__ double fixed_sum256(const double* src, int n, double* red, int t) {
-  auto ld = [&](int k) { return COHERENT ? load_sc1(src + k) : src[k]; };
+// Fixed-order sum of n doubles by the NT threads of a block (red[NT] in
+// LDS); the result is in thread 0's return value.  Eight independent
+// accumulators keep eight loads in flight per thread; the association is
+// fixed (bitwise reproducible).  Every thread of the block must call it.
+template <int NT>
+__device__ __forceinline__ double fixed_sum(const double* src, int n, double* red, int t) {
   double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   int k = t;
-  for (; k + 7 * 256 < n; k += 8 * 256) {
+  for (; k + 7 * NT < n; k += 8 * NT) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += ld(k + j * 256);
+    for (int j = 0; j < 8; ++j) acc[j] += src[k + j * NT];
   }
-  for (; k < n; k += 256) acc[0] += ld(k);
+  for (; k < n; k += NT) acc[0] += src[k];
   red[t] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
+  for (int h = NT / 2; h > 0; h >>= 1) {
     if (t < h) red[t] += red[t + h];
     __syncthreads();
   }
