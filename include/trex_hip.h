@@ -353,6 +353,25 @@ int trex_sankoff_ragged_backtrack(const int32_t* plan, int B, int64_t items, int
                                   int8_t* anc_states, void* stream);
 
 /* ========================================================================
+ * Synthetic data on the device: trex's
+ * generate_groundtruth (src/trex/ground_truth.py:112-197, mutate :20-52) and
+ * iid uniform leaf states, from a counter-based generator (splitmix64 of
+ * (seed, stream, counter); trex's JAX threefry streams cannot be
+ * reproduced, the process can).  Restated in oracle/datagen_ref.py.
+ *   seqs int8 [2 n_leaves - 1][L] out: root (last row) zero, every child =
+ *     its parent with exactly n_mutations distinct sites moved by
+ *     1 + U{0..Q-2} (mod Q); balanced numbering (children of parent p are
+ *     2(p - n_leaves), 2(p - n_leaves) + 1).  n_leaves a power of 2.
+ *   workspace trex_datagen_workspace_bytes(n_leaves, n_mutations) bytes.
+ * ---------------------------------------------------------------------- */
+int64_t trex_datagen_workspace_bytes(int n_leaves, int n_mutations);
+int trex_datagen_groundtruth(uint64_t seed, int n_leaves, int L, int Q, int n_mutations,
+                             int8_t* seqs, void* workspace, int64_t workspace_bytes,
+                             void* stream);
+/* out int8 [n]: uniform states in [0, Q) */
+int trex_datagen_uniform_states(uint64_t seed, int64_t n, int Q, int8_t* out, void* stream);
+
+/* ========================================================================
  * NK landscape-aware loss (src/trex/evals/benchmark.py): the parental
  * guidance term of _compute_loss_landscape_aware_stacked (:235-306) on top
  * of the surrogate cost, with compute_parental_logits (:586-663).

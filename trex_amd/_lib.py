@@ -98,6 +98,11 @@ SIGNATURES = {
                                          _c_f, _c_f, _c_f, _p, _p]),
     "trex_adam_seq_step": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_f, _p, _p, _p, _c_i, _c_f, _c_f,
                                   _c_f, _c_f, _p, _p]),
+    # synthetic data on the device
+    "trex_datagen_workspace_bytes": (_c_i64, [_c_i, _c_i]),
+    "trex_datagen_groundtruth": (_c_i, [ctypes.c_uint64, _c_i, _c_i, _c_i, _c_i, _p, _p, _c_i64,
+                                        _p]),
+    "trex_datagen_uniform_states": (_c_i, [ctypes.c_uint64, _c_i64, _c_i, _p, _p]),
 }
 
 

@@ -1,0 +1,143 @@
+// libtrexhip.so -- synthetic data on the device:
+// trex's ground-truth generator (src/trex/ground_truth.py:20-52 mutate,
+// :112-197 generate_groundtruth) and iid uniform leaf states, so C4 / C5-size
+// alignments are produced where they are consumed instead of on the host.
+//
+// Same process as the reference, different random numbers: trex draws with
+// JAX's threefry PRNG (not available here); this file uses a counter-based
+// generator, r(seed, stream, counter) = mix(seed ^ mix(stream << 32 | counter))
+// with mix = the splitmix64 finaliser, so every draw is a pure function of
+// its indices (no state, any launch shape, bitwise reproducible; restated in
+// numpy in oracle/datagen_ref.py, which the tests match bit for bit).
+//
+//   mutate(parent -> child): exactly n_mutations distinct sites (Floyd's
+//     sampling without replacement, draws on stream 2*child+1) get
+//     (x + 1 + r % (Q - 1)) mod Q (stream 2*child, counter = site);
+//   generate_groundtruth: a balanced tree, root (last row) all zero, parents
+//     processed from the root down (parent n_all-1-i has children 2(p-nl)
+//     and 2(p-nl)+1, ground_truth.py:165-178), one launch per tree level.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "trex_common.h"
+
+namespace trex {
+
+namespace {
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__host__ __device__ __forceinline__ uint64_t draw(uint64_t seed, uint64_t stream, uint64_t counter) {
+  return mix64(seed ^ mix64((stream << 32) | (counter & 0xFFFFFFFFull)));
+}
+
+constexpr int kMaxMut = 1024;  // sites per child held in LDS
+
+// Floyd's algorithm: n_mut distinct sites of [0, L) per child (one thread
+// per child; n_mut is small: trex uses 1-50 mutations per edge)
+__global__ void choose_sites_kernel(uint64_t seed, int L, int n_mut, int child0, int nchild,
+                                    int* __restrict__ sites) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nchild) return;
+  const int child = child0 + t;
+  int* s = sites + (size_t)t * n_mut;
+  int k = 0;
+  for (int j = L - n_mut; j < L; ++j) {
+    const int r = (int)(draw(seed, 2ull * child + 1, (uint64_t)j) % (uint64_t)(j + 1));
+    bool seen = false;
+    for (int q = 0; q < k; ++q) seen |= s[q] == r;
+    s[k++] = seen ? j : r;
+  }
+}
+
+// one tree level: children [child0, child0 + nchild) from their parents
+__global__ __launch_bounds__(256) void mutate_level_kernel(uint64_t seed, int nl, int L, int Q,
+                                                           int n_mut, int child0,
+                                                           const int* __restrict__ sites,
+                                                           int8_t* __restrict__ seqs) {
+  __shared__ int ms[kMaxMut];
+  const int t = blockIdx.y;
+  const int child = child0 + t;
+  const int parent = nl + child / 2;  // children 2(p - nl), 2(p - nl) + 1
+  for (int q = threadIdx.x; q < n_mut; q += blockDim.x) ms[q] = sites[(size_t)t * n_mut + q];
+  __syncthreads();
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= L) return;
+  bool hit = false;
+  for (int q = 0; q < n_mut; ++q) hit |= ms[q] == s;
+  int x = seqs[(size_t)parent * L + s];
+  if (hit) x = (x + 1 + (int)(draw(seed, 2ull * child, (uint64_t)s) % (uint64_t)(Q - 1))) % Q;
+  seqs[(size_t)child * L + s] = (int8_t)x;
+}
+
+__global__ __launch_bounds__(256) void uniform_states_kernel(uint64_t seed, int64_t n, int Q,
+                                                             int8_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (int8_t)(draw(seed, (uint64_t)(i >> 32) + 0x100000000ull, (uint64_t)i) % (uint64_t)Q);
+}
+
+}  // namespace
+
+}  // namespace trex
+
+using namespace trex;
+
+extern "C" int64_t trex_datagen_workspace_bytes(int n_leaves, int n_mutations) {
+  if (n_leaves <= 0 || n_mutations < 0) return 0;
+  return (int64_t)n_leaves * (n_mutations > 0 ? n_mutations : 1) * 4 + 256;
+}
+
+extern "C" int trex_datagen_groundtruth(uint64_t seed, int n_leaves, int L, int Q, int n_mutations,
+                                        int8_t* seqs, void* workspace, int64_t workspace_bytes,
+                                        void* stream) {
+  const char* fn = "trex_datagen_groundtruth";
+  if (n_leaves < 2 || (n_leaves & (n_leaves - 1)) != 0)
+    return set_error(TREX_E_ARG, "%s: n_leaves must be a power of 2 (got %d)", fn, n_leaves);
+  if (L <= 0 || Q < 2 || Q > 127 || n_mutations < 0 || n_mutations > L || n_mutations > kMaxMut ||
+      !seqs || !workspace)
+    return set_error(TREX_E_ARG, "%s: bad arguments (L=%d Q=%d n_mutations=%d)", fn, L, Q,
+                     n_mutations);
+  if (workspace_bytes < trex_datagen_workspace_bytes(n_leaves, n_mutations))
+    return set_error(TREX_E_ARG, "%s: workspace too small", fn);
+  const int nl = n_leaves, n_all = 2 * nl - 1;
+  hipStream_t st = (hipStream_t)stream;
+  // the root (last row) is all zero (ground_truth.py:160)
+  if (hipMemsetAsync(seqs + (size_t)(n_all - 1) * L, 0, (size_t)L, st) != hipSuccess)
+    return set_error(TREX_E_HIP, "%s: memset failed", fn);
+  int* sites = static_cast<int*>(workspace);
+  // parents i = 0 .. n_anc-1 from the root down; depth d holds i in
+  // [2^d - 1, 2^(d+1) - 1), whose children are a contiguous block of rows
+  for (int lo = 0, width = 1; lo < nl - 1; lo += width, width *= 2) {
+    const int hi = lo + width;                 // parents i in [lo, hi)
+    const int p_lo = n_all - hi, p_hi = n_all - lo;  // parent rows [p_lo, p_hi)
+    const int child0 = 2 * (p_lo - nl), nchild = 2 * (p_hi - p_lo);
+    if (n_mutations > 0)
+      hipLaunchKernelGGL(choose_sites_kernel, dim3((nchild + 63) / 64), dim3(64), 0, st, seed, L,
+                         n_mutations, child0, nchild, sites);
+    hipLaunchKernelGGL(mutate_level_kernel, dim3((L + 255) / 256, nchild), dim3(256), 0, st, seed,
+                       nl, L, Q, n_mutations, child0, sites, seqs);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return TREX_OK;
+}
+
+extern "C" int trex_datagen_uniform_states(uint64_t seed, int64_t n, int Q, int8_t* out,
+                                           void* stream) {
+  if (n <= 0 || Q < 1 || Q > 127 || !out)
+    return set_error(TREX_E_ARG, "trex_datagen_uniform_states: bad arguments");
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(uniform_states_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)),
+                     dim3(256), 0, (hipStream_t)stream, seed, n, Q, out);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return set_error(TREX_E_HIP, "trex_datagen_uniform_states: %s", hipGetErrorString(e));
+  return TREX_OK;
+}

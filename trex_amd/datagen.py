@@ -154,3 +154,50 @@ def generate_tree_data(landscape: dict, adjacency, root_sequence, mutation_rate:
         seqs[node] = seq
     return PhylogeneticTree(np.zeros((n, L), np.float32), seqs.astype(np.float32),
                             A.astype(np.float32))
+
+
+# ---------------------------------------------------------------------------
+# Device generators (libtrexhip.so, trex_amd/csrc/datagen.hip): the same
+# ground-truth process run where the data are consumed, so C4/C5-size inputs
+# never cross PCIe.  Random numbers come from a counter-based generator
+# (splitmix64 of (seed, stream, counter)); oracle/datagen_ref.py computes them
+# bit for bit on the CPU.
+
+
+def generate_groundtruth_device(n_leaves: int, n_states: int, n_mutations: int, seq_length: int,
+                                seed: int = 42, device="cuda"):
+    """generate_groundtruth's process on the device: returns (all_sequences
+    int8 (2 n_leaves - 1, seq_length) on `device`, adjacency float32 numpy),
+    same numbering as the host version (leaves first, root last)."""
+    import torch
+
+    from ._lib import check, lib, ptr, stream_handle
+
+    if not (n_leaves > 1 and (n_leaves & (n_leaves - 1)) == 0):
+        raise ValueError("n_leaves must be a power of 2 (and > 1).")
+    dev = torch.device(device)
+    n_all = 2 * n_leaves - 1
+    seqs = torch.empty((n_all, seq_length), dtype=torch.int8, device=dev)
+    ws = torch.empty(int(lib().trex_datagen_workspace_bytes(n_leaves, n_mutations)),
+                     dtype=torch.uint8, device=dev)
+    check(lib().trex_datagen_groundtruth(seed & (2**64 - 1), n_leaves, seq_length, n_states,
+                                         n_mutations, ptr(seqs), ptr(ws), ws.numel(),
+                                         stream_handle(dev)))
+    adj = np.zeros((n_all, n_all), dtype=np.float32)
+    i = np.arange(n_leaves - 1)
+    adj[2 * i, n_leaves + i] = 1
+    adj[2 * i + 1, n_leaves + i] = 1
+    return seqs, adj
+
+
+def uniform_states_device(shape, n_states: int, seed: int = 0, device="cuda"):
+    """iid uniform states in [0, n_states), int8 tensor of `shape` on `device`."""
+    import torch
+
+    from ._lib import check, lib, ptr, stream_handle
+
+    out = torch.empty(shape, dtype=torch.int8, device=torch.device(device))
+    if out.numel():
+        check(lib().trex_datagen_uniform_states(seed & (2**64 - 1), out.numel(), n_states,
+                                                ptr(out), stream_handle(out.device)))
+    return out
