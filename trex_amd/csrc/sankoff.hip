@@ -740,7 +740,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         for (int s = 0; s < SPT; ++s) tot += (double)score[s];
         if (A.site_score) st<SPT>(A.site_score + site_base + site, score);
       }
-      tot = wave_sum(tot);
+      tot = wave_sum_lane0(tot);
       if (lane == 0) A.part_tree[item] = tot;
     }
 
@@ -911,15 +911,28 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
       }
 
       // ---- per-item dC partial (fixed-order reduce kernel sums the items) ----
+      if constexpr (Q == 4) {
+        double v16[16];
 #pragma unroll
-      for (int i = 0; i < Q; ++i)
+        for (int i = 0; i < Q; ++i)
 #pragma unroll
-        for (int j = 0; j < Q; ++j) {
-          double v = (double)acc[i][j];
-          if constexpr (MODE == kSoftK) v = v * (double)cf.k[i][j];
-          v = wave_sum(v);
-          if (lane == 0) A.part_dc[(size_t)(i * Q + j) * nb + item] = v;
-        }
+          for (int j = 0; j < Q; ++j) {
+            v16[i * Q + j] = (double)acc[i][j];
+            if constexpr (MODE == kSoftK) v16[i * Q + j] *= (double)cf.k[i][j];
+          }
+        const double v = wave_reduce_scatter16(v16, lane);
+        if ((lane & 3) == 0) A.part_dc[(size_t)(lane >> 2) * nb + item] = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < Q; ++i)
+#pragma unroll
+          for (int j = 0; j < Q; ++j) {
+            double v = (double)acc[i][j];
+            if constexpr (MODE == kSoftK) v = v * (double)cf.k[i][j];
+            v = wave_sum_lane0(v);
+            if (lane == 0) A.part_dc[(size_t)(i * Q + j) * nb + item] = v;
+          }
+      }
     }
     item += stride;
   } while (PERSIST && item < item_end);

@@ -64,6 +64,66 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// ---- cross-lane sums without LDS: v_permlane32_swap / v_permlane16_swap
+// (gfx950) for the two upper butterfly levels, DPP row / quad permutations
+// inside a 16-lane row.  Fixed pairing: bitwise reproducible. ----
+__device__ __forceinline__ double dbl(uint32_t lo, uint32_t hi) {
+  return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ uint32_t lo32(double v) { return (uint32_t)__double2loint(v); }
+__device__ __forceinline__ uint32_t hi32(double v) { return (uint32_t)__double2hiint(v); }
+// x, y -> (lanes < 32: x[l] + x[l + 32]; lanes >= 32: y[l - 32] + y[l])
+__device__ __forceinline__ double swap32_add(double x, double y) {
+  const auto a = __builtin_amdgcn_permlane32_swap(lo32(x), lo32(y), false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi32(x), hi32(y), false, false);
+  return dbl(a[0], b[0]) + dbl(a[1], b[1]);
+}
+// x, y -> rows (16 lanes) 0, 2: x summed over row pairs (0,1), (2,3); rows 1, 3: y
+__device__ __forceinline__ double swap16_add(double x, double y) {
+  const auto a = __builtin_amdgcn_permlane16_swap(lo32(x), lo32(y), false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi32(x), hi32(y), false, false);
+  return dbl(a[0], b[0]) + dbl(a[1], b[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  return dbl((uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo32(v), CTRL, 0xF, 0xF, false),
+             (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi32(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppRowRor8 = 0x128, kDppHalfMirror = 0x141, kDppQuadX1 = 0xB1, kDppQuadX2 = 0x4E;
+
+// sum over the wave; lane 0 (every lane of quad 0, in fact) holds the total
+__device__ __forceinline__ double wave_sum_lane0(double v) {
+  v = swap32_add(v, v);
+  v = swap16_add(v, v);
+  v += dpp_d<kDppRowRor8>(v);
+  v += dpp_d<kDppHalfMirror>(v);
+  v += dpp_d<kDppQuadX2>(v);
+  v += dpp_d<kDppQuadX1>(v);
+  return v;
+}
+
+// reduce-scatter of 16 per-lane values: lane l returns the wave total of
+// v[(l >> 2) & 15] (62 VALU ops instead of 16 full butterflies)
+__device__ __forceinline__ double wave_reduce_scatter16(const double (&v)[16], int lane) {
+  double w[8], z[4], y[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = swap32_add(v[k], v[k + 8]);  // index k + 8 (l >> 5)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) z[k] = swap16_add(w[k], w[k + 4]);  // index k + 4 (l >> 4)
+  const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // partner l ^ 8: index k + 2 b3 + 4 (l >> 4)
+    const double keep = b3 ? z[k + 2] : z[k], send = b3 ? z[k] : z[k + 2];
+    y[k] = keep + dpp_d<kDppRowRor8>(send);
+  }
+  // partner: the mirror lane in the 8-lane half row (opposite b2)
+  const double keep = b2 ? y[1] : y[0], send = b2 ? y[0] : y[1];
+  double x = keep + dpp_d<kDppHalfMirror>(send);
+  x += dpp_d<kDppQuadX2>(x);
+  x += dpp_d<kDppQuadX1>(x);
+  return x;
+}
+
 __device__ __forceinline__ void store_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
