@@ -366,3 +366,32 @@ def test_adam_seq_step_fused_is_bitwise_separate(device, Q, L):
                                 3, 0.01, 0.9, 0.999, 1e-8, ptr(gb), st))
     assert torch.equal(g, gb) and torch.equal(pa, pb) and torch.equal(ma, mb)
     assert torch.equal(va, vb)
+
+
+@pytest.mark.parametrize("N,K,skip,x3", [(511, 4096, 0, True), (300, 8192, 128, True),
+                                         (511, 4096, 0, False), (200, 1024, 0, False)])
+def test_gram_is_run_to_run_deterministic(device, N, K, skip, x3):
+    """The split-K Grams give bitwise the same symmetric G on every run: the
+    reduce writes each mirrored pair of a diagonal tile from one thread only
+    (two threads holding the (i, j) and (j, i) partial sums used to race)."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    rng = np.random.default_rng(N + K)
+    x = rng.normal(size=(N, K // 4, 4)) * 3
+    e = np.exp(x - x.max(-1, keepdims=True))
+    S = _t((e / e.sum(-1, keepdims=True)).reshape(N, K), device)
+    st = stream_handle(torch.device(device))
+    ws = torch.empty(int(lib().trex_tree_workspace_bytes(N, K)), dtype=torch.uint8, device=device)
+    runs = []
+    for _ in range(4):
+        G = torch.empty((N, N), device=device)
+        if x3:
+            check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, skip, 1.0, ptr(G), ptr(ws),
+                                               ws.numel(), st))
+        else:
+            check(lib().trex_tree_gram_skip(ptr(S), N, K, skip, ptr(G), ptr(ws), ws.numel(), st))
+        runs.append(G)
+    t0 = (skip // 64) * 64
+    for G in runs[1:]:
+        assert torch.equal(G[t0:], runs[0][t0:])
+    assert torch.equal(runs[0][t0:, t0:], runs[0][t0:, t0:].T)

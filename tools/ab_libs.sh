@@ -1,0 +1,19 @@
+#!/bin/bash
+# A/B the C4 bench line across library builds on the same box.
+# usage: tools/ab_libs.sh lib1.so lib2.so ... (reps via REPS, bench flags via BENCH_ARGS)
+cd "$(dirname "$0")/.."
+ARGS=${BENCH_ARGS:---no-cpu-baseline --no-c5 --no-c2 --no-c3 --no-nk --no-ragged --steps 20}
+for rep in $(seq ${REPS:-2}); do
+  for lib in "$@"; do
+    TREX_HIP_LIB=$lib timeout -k 10 200 python bench.py $ARGS > gpurun_out/ab.json || exit 1
+    python -c "
+import json,sys
+d=json.load(open(sys.argv[1]))
+extra = ''
+if 'c4_shard' in d: extra += ' shard %.1f us' % d['c4_shard']['fused_kernel_us']
+if 'c2' in d: extra += ' c2 %.1f us' % (d['c2']['ms_per_step']*1e3)
+if 'c3' in d: extra += ' c3 soft %.1f us hard %.1f us' % (d['c3']['soft_ms_per_step']*1e3, d['c3']['hard_recon_ms_per_step']*1e3)
+if 'c5' in d: extra += ' c5 %.3f ms' % d['c5']['ms_per_step']
+print(sys.argv[2], round(d['value']/1e9,1), d['roofline']['per_kernel_us'], extra)" gpurun_out/ab.json "$lib"
+  done
+done

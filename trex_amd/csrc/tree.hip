@@ -422,7 +422,9 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(const float* __restric
     double s = 0.0;
     for (int sp = 0; sp < ksplit; ++sp) s += (double)part[((size_t)sp * npairs + pair) * 4096 + e];
     const int i = ti * 64 + e / 64, j = tj * 64 + e % 64;
-    if (i < N && j < N) {
+    // a diagonal tile holds both (i, j) and (j, i): only i <= j writes the
+    // pair, or two threads would race on it with differently rounded sums
+    if (i < N && j < N && (!symmetric || ti != tj || i <= j)) {
       G[(size_t)i * N + j] = (float)s;
       if (symmetric) G[(size_t)j * N + i] = (float)s;
     }
@@ -598,7 +600,8 @@ __global__ __launch_bounds__(256) void gram3_reduce_kernel(const float* __restri
   int si, sj;
   pair_tiles(tile, ns, 1, t0s, &si, &sj);
   const int i = si * 32 + (e >> 5), j = sj * 32 + (e & 31);
-  if (i < N && j < N) {
+  // diagonal tiles: only i <= j writes the mirrored pair (no write race)
+  if (i < N && j < N && (si != sj || i <= j)) {
     G[(size_t)i * N + j] = (float)s;
     G[(size_t)j * N + i] = (float)s;
   }
