@@ -3,11 +3,12 @@
 
 One step = softmin Sankoff forward (writes the DP table, as trex's run_sankoff
 returns it) + adjoint sweep (d score / d cost) over this rank's shard of the
-C4 workload (BASELINE.json configs[3]: random 32-taxa topologies x 5000 sites
-x 4 states, tau = 0.5), then an RCCL all-reduce of [d_cost, loss] when N > 1.
-Weak scaling: each rank owns --trees-per-gpu trees (default 128, so N = 8 is
-exactly C4's 1024 trees).  Metric: site-node-state updates/s = B*L*n_int*Q per
-step over all ranks.
+C4 workload (BASELINE.json configs[3]: 1024 random 32-taxa topologies x 5000
+sites x 4 states, tau = 0.5), then an RCCL all-reduce of [d_cost, loss] when
+N > 1.  Strong scaling: the N ranks split C4's 1024 trees (--trees) in
+contiguous blocks, so N = 1 runs the whole batch and N = 8 runs 128 trees per
+rank.  Metric: site-node-state updates/s = B*L*n_int*Q per step over all
+ranks.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
