@@ -370,6 +370,29 @@ int trex_datagen_groundtruth(uint64_t seed, int n_leaves, int L, int Q, int n_mu
                              void* stream);
 /* out int8 [n]: uniform states in [0, Q) */
 int trex_datagen_uniform_states(uint64_t seed, int64_t n, int Q, int8_t* out, void* stream);
+/* nk_model.generate_tree_data (src/trex/nk_model.py:116-278): NK-model
+ * sequence evolution along a tree, branch_length Metropolis steps per edge
+ * (coupled redraw of a site and its K interactions with probability
+ * coupled_prob, else per-site Bernoulli(rate) redraws; rate =
+ * min(mutation_rate exp(N(0,1) noise_std), 1) per edge; accepted with
+ * probability min(1, exp(f_new - f_cur)), f = mean site fitness).  Same
+ * counter-based draws as above (restated in oracle/datagen_ref.py).
+ *   interactions int32 [L][K], fitness f32 [L][Q^(K+1)] (device)
+ *   parent int32 [n_nodes] (device); order int32 [n_slots] (device): the
+ *     reference's BFS sorted_nodes -- root first, then each level, and the
+ *     node n_nodes - 1 repeated for every slot the BFS did not fill (its -1
+ *     index, nk_model.py:186-190, 236-245; trex_amd.datagen.bfs_levels
+ *     builds it); level_offsets int32 [n_levels + 1] (HOST array): slots
+ *     [level_offsets[lv], level_offsets[lv + 1]) run in one launch, so each
+ *     level's nodes must have their parents in earlier levels; slot s
+ *     draws from streams 4s .. 4s + 3
+ *   seqs int8 [n_nodes][L] in/out: the root row holds the root sequence;
+ *     every other row is written.  L <= 65536, Q^(K+1) < 2^31. */
+int trex_datagen_nk_tree(uint64_t seed, int n_nodes, int L, int Q, int K, const int* interactions,
+                         const float* fitness, const int* parent, const int* order,
+                         const int* level_offsets, int n_levels, float mutation_rate,
+                         float noise_std, float coupled_prob, int branch_length, int8_t* seqs,
+                         void* stream);
 
 /* ========================================================================
  * NK landscape-aware loss (src/trex/evals/benchmark.py): the parental

@@ -103,6 +103,8 @@ SIGNATURES = {
     "trex_datagen_groundtruth": (_c_i, [ctypes.c_uint64, _c_i, _c_i, _c_i, _c_i, _p, _p, _c_i64,
                                         _p]),
     "trex_datagen_uniform_states": (_c_i, [ctypes.c_uint64, _c_i64, _c_i, _p, _p]),
+    "trex_datagen_nk_tree": (_c_i, [ctypes.c_uint64, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _p, _p, _c_i,
+                                    _c_f, _c_f, _c_f, _c_i, _p, _p]),
 }
 
 

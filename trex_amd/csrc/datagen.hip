@@ -83,6 +83,101 @@ __global__ __launch_bounds__(256) void uniform_states_kernel(uint64_t seed, int6
     out[i] = (int8_t)(draw(seed, (uint64_t)(i >> 32) + 0x100000000ull, (uint64_t)i) % (uint64_t)Q);
 }
 
+// ---- NK-model evolution along a tree (nk_model.py:116-278) ---------------
+// One workgroup per node of a BFS level (its parent is finished): the
+// parent's sequence in LDS, then branch_length Metropolis steps, each a
+// coupled (one site + its K interactions) or independent (per-site
+// Bernoulli(rate)) redraw, accepted with probability min(1, exp(f_new -
+// f_cur)).  Fitness = mean over sites of fitness[i][sum_j s(site_j) Q^j]
+// (site_0 = i, site_j = interactions[i][j - 1]), summed in 2^-40 fixed
+// point (int64: order-free, bitwise reproducible).  Draws per BFS slot n
+// (the reference's sorted_nodes index): stream 4n: rate noise (2
+// uniforms), stream 4n + 1: step b's coupled decision / site / acceptance
+// (counters 4b .. 4b + 2), stream 4n + 2: new states (counter b L + i),
+// stream 4n + 3: independent-mutation mask.
+__device__ __forceinline__ double unit53(uint64_t r) { return (double)(r >> 11) * 0x1.0p-53; }
+__device__ __forceinline__ float unit24(uint64_t r) { return (float)(r >> 40) * 0x1.0p-24f; }
+
+__device__ __forceinline__ int64_t nk_fixed(float v) { return (int64_t)((double)v * 0x1.0p40); }
+
+template <int BS>
+__device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  int64_t t = 0;
+  for (int i = 0; i < BS / 64; ++i) t += red[i];
+  return t;
+}
+
+template <int BS>
+__device__ int64_t nk_fitness_fixed(const int8_t* seq, int L, int Q, int K,
+                                    const int* __restrict__ inter, const float* __restrict__ fit,
+                                    int64_t tw, int64_t* red) {
+  int64_t acc = 0;
+  for (int i = threadIdx.x; i < L; i += BS) {
+    int64_t idx = seq[i];
+    int64_t pw = Q;
+    for (int j = 0; j < K; ++j, pw *= Q) idx += (int64_t)seq[inter[(size_t)i * K + j]] * pw;
+    acc += nk_fixed(fit[(size_t)i * tw + idx]);
+  }
+  return block_sum_i64<BS>(acc, red);
+}
+
+constexpr int kNkBlock = 256;
+
+__global__ __launch_bounds__(kNkBlock) void nk_evolve_level_kernel(
+    uint64_t seed, const int* __restrict__ order, int slot0, const int* __restrict__ parent, int L,
+    int Q,
+    int K, const int* __restrict__ inter, const float* __restrict__ fit, int64_t tw,
+    float mutation_rate, float noise_std, float coupled_prob, int branch_length,
+    int8_t* __restrict__ seqs) {
+  extern __shared__ __attribute__((aligned(16))) int8_t nk_lds[];
+  __shared__ int64_t red[kNkBlock / 64];
+  int8_t* cur = nk_lds;
+  int8_t* prop = nk_lds + L;
+  const int slot = slot0 + (int)blockIdx.x;
+  const int node = order[slot];
+  const int par = parent[node];
+  const uint64_t sb = 4ull * (uint64_t)slot;
+  for (int i = threadIdx.x; i < L; i += kNkBlock) cur[i] = seqs[(size_t)par * L + i];
+  __syncthreads();
+  float rate = fminf(mutation_rate, 1.0f);
+  if (noise_std != 0.0f) {  // rate * exp(N(0, 1) * std), Box-Muller
+    const double u1 = 1.0 - unit53(draw(seed, sb, 0)), u2 = unit53(draw(seed, sb, 1));
+    const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+    rate = fminf((float)((double)mutation_rate * exp(z * (double)noise_std)), 1.0f);
+  }
+  int64_t fcur = nk_fitness_fixed<kNkBlock>(cur, L, Q, K, inter, fit, tw, red);
+  for (int b = 0; b < branch_length; ++b) {
+    const bool coupled = unit24(draw(seed, sb + 1, 4ull * b)) < coupled_prob;
+    const int site0 = (int)(draw(seed, sb + 1, 4ull * b + 1) % (uint64_t)L);
+    for (int i = threadIdx.x; i < L; i += kNkBlock) {
+      bool m;
+      if (coupled) {
+        m = i == site0;
+        for (int j = 0; j < K; ++j) m |= inter[(size_t)site0 * K + j] == i;
+      } else {
+        m = unit24(draw(seed, sb + 3, (uint64_t)b * L + i)) < rate;
+      }
+      const int v = (int)(draw(seed, sb + 2, (uint64_t)b * L + i) % (uint64_t)Q);
+      prop[i] = m ? (int8_t)v : cur[i];
+    }
+    __syncthreads();
+    const int64_t fprop = nk_fitness_fixed<kNkBlock>(prop, L, Q, K, inter, fit, tw, red);
+    const double delta = (double)(fprop - fcur) * 0x1.0p-40 / (double)L;
+    const bool accept = delta >= 0.0 || unit53(draw(seed, sb + 1, 4ull * b + 2)) < exp(delta);
+    if (accept) {
+      for (int i = threadIdx.x; i < L; i += kNkBlock) cur[i] = prop[i];
+      fcur = fprop;
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < L; i += kNkBlock) seqs[(size_t)node * L + i] = cur[i];
+}
+
 }  // namespace
 
 }  // namespace trex
@@ -139,5 +234,40 @@ extern "C" int trex_datagen_uniform_states(uint64_t seed, int64_t n, int Q, int8
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)
     return set_error(TREX_E_HIP, "trex_datagen_uniform_states: %s", hipGetErrorString(e));
+  return TREX_OK;
+}
+
+extern "C" int trex_datagen_nk_tree(uint64_t seed, int n_nodes, int L, int Q, int K,
+                                    const int* interactions, const float* fitness,
+                                    const int* parent, const int* order, const int* level_offsets,
+                                    int n_levels, float mutation_rate, float noise_std,
+                                    float coupled_prob, int branch_length, int8_t* seqs,
+                                    void* stream) {
+  const char* fn = "trex_datagen_nk_tree";
+  if (n_nodes < 1 || L < 1 || L > 65536 || Q < 2 || Q > 127 || K < 0 || K > 16 || !fitness ||
+      (K > 0 && !interactions) || !parent || !order || !level_offsets || n_levels < 1 || !seqs ||
+      branch_length < 0 || !finite_f32(mutation_rate) || !finite_f32(noise_std) ||
+      !finite_f32(coupled_prob))
+    return set_error(TREX_E_ARG, "%s: bad arguments", fn);
+  double tw = 1.0;
+  for (int j = 0; j <= K; ++j) tw *= Q;
+  if (tw > 2147483647.0) return set_error(TREX_E_ARG, "%s: Q^(K+1) too large", fn);
+  const int lds = 2 * L;
+  if (lds > 65536 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(nk_evolve_level_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    return set_error(TREX_E_HIP, "%s: LDS size", fn);
+  hipStream_t st = (hipStream_t)stream;
+  // level 0 is the root (copied in by the caller); host-side offsets; a
+  // level's nodes are independent (their parents are done)
+  for (int lv = 1; lv < n_levels; ++lv) {
+    const int lo = level_offsets[lv], hi = level_offsets[lv + 1];
+    if (hi <= lo) continue;
+    hipLaunchKernelGGL(nk_evolve_level_kernel, dim3(hi - lo), dim3(kNkBlock), lds, st, seed,
+                       order, lo, parent, L, Q, K, interactions, fitness, (int64_t)tw,
+                       mutation_rate, noise_std, coupled_prob, branch_length, seqs);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
   return TREX_OK;
 }

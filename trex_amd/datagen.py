@@ -201,3 +201,69 @@ def uniform_states_device(shape, n_states: int, seed: int = 0, device="cuda"):
         check(lib().trex_datagen_uniform_states(seed & (2**64 - 1), out.numel(), n_states,
                                                 ptr(out), stream_handle(out.device)))
     return out
+
+
+def bfs_levels(adjacency):
+    """generate_tree_data's traversal (nk_model.py:149-190) as launch levels:
+    parent = argmax of each adjacency row, root = the first self-parented
+    node (0 when there is none, the jnp.where fill), BFS from it.  Returns
+    (root, parent, order, offsets): ``order`` is the reference's
+    sorted_nodes with its unfilled -1 slots resolved as the reference's
+    indexing does (the last node), ``offsets`` the launch levels -- BFS
+    levels for the reached nodes, then one slot per level for the -1 tail
+    (each re-evolves the last node from its parent, in sequence)."""
+    A = np.asarray(adjacency)
+    n = A.shape[0]
+    parent = np.argmax(A, axis=1).astype(np.int32)
+    roots = np.nonzero(parent == np.arange(n))[0]
+    root = int(roots[0]) if roots.size else 0
+    order, offsets, frontier, seen = [], [0], [root], {root}
+    while frontier:
+        order.extend(frontier)
+        offsets.append(len(order))
+        nxt = []
+        for node in frontier:
+            for c in np.nonzero(A[:, node] == 1)[0]:
+                c = int(c)
+                if c not in seen:
+                    seen.add(c)
+                    nxt.append(c)
+        frontier = nxt
+    # -1 slots index node n - 1; the reference leaves it alone when it is the
+    # root (node_index == root_node), otherwise re-evolves it once per slot
+    while len(order) < n and root != n - 1:
+        order.append(n - 1)
+        offsets.append(len(order))
+    return root, parent, np.asarray(order, np.int32), np.asarray(offsets, np.int32)
+
+
+def generate_tree_data_device(landscape: dict, adjacency, root_sequence, mutation_rate: float,
+                              seed: int = 0, coupled_mutation_prob: float = 0.5,
+                              n_states: int = 20, mutation_rate_noise_std: float = 0.0,
+                              branch_length: int = 1, device="cuda"):
+    """generate_tree_data's process on the device (trex_datagen_nk_tree):
+    returns the (n_nodes, L) int8 sequences on ``device`` (every node in BFS
+    order evolved from its parent; the root row is root_sequence)."""
+    import torch
+
+    from ._lib import check, lib, ptr, stream_handle
+
+    if "n_states" in landscape:
+        n_states = int(landscape["n_states"])
+    dev = torch.device(device)
+    root, parent, order, offsets = bfs_levels(adjacency)
+    inter = np.asarray(landscape["interactions"], np.int32)
+    fit = np.asarray(landscape["fitness_tables"], np.float32)
+    L = int(np.asarray(root_sequence).reshape(-1).shape[0])
+    K = int(inter.shape[1]) if inter.ndim == 2 else 0
+    n = parent.shape[0]
+    seqs = torch.zeros((n, L), dtype=torch.int8, device=dev)
+    seqs[root] = torch.as_tensor(np.asarray(root_sequence).reshape(-1).astype(np.int8), device=dev)
+    t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
+    inter_d, fit_d, par_d, ord_d = t(inter), t(fit), t(parent), t(order)
+    check(lib().trex_datagen_nk_tree(seed & (2**64 - 1), n, L, n_states, K, ptr(inter_d),
+                                     ptr(fit_d), ptr(par_d), ptr(ord_d), offsets.ctypes.data,
+                                     len(offsets) - 1, float(mutation_rate),
+                                     float(mutation_rate_noise_std), float(coupled_mutation_prob),
+                                     int(branch_length), ptr(seqs), stream_handle(dev)))
+    return seqs
