@@ -97,12 +97,18 @@ def test_batched_hard_fwd_grad_wide(device, L, Q, n):
     np.testing.assert_allclose(_sm(mg), ref["marginals"], rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("Q", [20, 7, 61])
-def test_backtrack_wide_matches_reference(device, Q):
+@pytest.mark.parametrize("bt", ["8", "4", "0"])
+@pytest.mark.parametrize("Q,ties", [(20, False), (20, True), (7, False), (5, True), (32, True),
+                                    (61, False)])
+def test_backtrack_wide_matches_reference(device, Q, ties, bt, monkeypatch):
+    """trex-exact states on every Q > 4 backtrack kernel: 8 or 4 lanes per
+    site (Q <= 32, TREX_BT4) and one lane per site; Hamming costs (ties:
+    the first-index argmin rule across the lanes' state ranges)."""
+    monkeypatch.setenv("TREX_BT4", bt)
     B, n, L = 3, 24, 515
     ch = random_topologies(B, n, seed=3 + Q)
     leaves = random_leaves(B, n, L, Q, seed=4 + Q)
-    cost = int_cost(Q, seed=5)
+    cost = hamming(Q) if ties else int_cost(Q, seed=5)
     eng = _engine(ch, L, Q, device)
     lv = _dev(leaves, device)
     c = _dev(cost, device, torch.float32)

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "sankoff_dev.h"
 #include "trex_common.h"
@@ -524,6 +525,110 @@ __global__ __launch_bounds__(kWave) void wide_backtrack_kernel(const int* __rest
   }
 }
 
+// Q <= 32, uniform batches: LPS = 8 (default) or 4 lanes per site (8 / 16
+// sites per wave).  Lane q of a site scans states [q * ch, q * ch + ch), ch
+// = ceil(Q / LPS), with trex's strict-< scan, and the site's lanes combine
+// (smaller value, then lower index) by DPP -- the first-index argmin of
+// sankoff.py:177-183, bit for bit.  8x the waves of the one-lane-per-site
+// kernel (C3: 1 250 instead of 157) and an eighth of its serial compare
+// chain per step; the parent states stay in LDS ([n_int][sites] bytes), the
+// next rows are prefetched four steps ahead (read as dwords: a wave's sites
+// are one contiguous span of each row)
+// partner lane for combine level m of a site's LPS lanes: quad xor 1, xor 2,
+// then the 8-lane half-row mirror (i <-> 7 - i: after the quad levels any
+// cross-quad pairing completes the reduction, the combine being symmetric)
+template <int M>
+__device__ __forceinline__ int bt_partner(int v) {
+  constexpr int ctrl = M == 1 ? 0xB1 : M == 2 ? 0x4E : 0x141;
+  return __builtin_amdgcn_update_dpp(0, v, ctrl, 0xF, 0xF, true);
+}
+template <int LPS>  // lanes per site: 4 or 8
+__global__ __launch_bounds__(kWave) void wide_backtrack4_kernel(const int* __restrict__ bt,
+                                                                const float* __restrict__ cost,
+                                                                const float* __restrict__ dp,
+                                                                int n_int, int L, int Q, int tiles,
+                                                                int8_t* __restrict__ anc) {
+  constexpr int kBtCh = 32 / LPS;  // max states per lane (Q <= 32)
+  constexpr int SPW = kWave / LPS;  // sites per wave
+  extern __shared__ __attribute__((aligned(16))) float bl[];
+  float* c = bl;                                          // [Q][Q] (32 x 32 reserved)
+  int8_t* sts = reinterpret_cast<int8_t*>(bl + 32 * 32);  // [n_int][SPW]
+  const int tree = blockIdx.x / tiles;
+  const int tile = blockIdx.x - tree * tiles;
+  const size_t rows_base = (size_t)tree * n_int * L;
+  const int lane = threadIdx.x;
+  for (int t = lane; t < 32 * 32; t += kWave) c[t] = t < Q * Q ? cost[t] : 0.0f;
+  __syncthreads();
+  const int sg = lane / LPS, q = lane % LPS;
+  const int site = tile * SPW + sg;
+  const bool live = site < L;  // no early exit: the quad combine needs every lane
+  const int ch = (Q + LPS - 1) / LPS;
+  const int j0 = q * ch;
+  const cptr<int> prog = as_const(bt) + (size_t)tree * n_int * 2;
+  const uint32_t rowbytes = (uint32_t)L * Q * 4;
+  const rsrc_t rdp = make_rsrc(dp + rows_base * Q, (uint32_t)n_int * rowbytes);
+  // lane offsets of its states; invalid states / dead sites read nothing
+  int voff[kBtCh];
+#pragma unroll
+  for (int t = 0; t < kBtCh; ++t)
+    voff[t] = (live && t < ch && j0 + t < Q) ? (site * Q + j0 + t) * 4 : 0x7FFFFFF0;
+  int8_t* at = anc + rows_base + (live ? site : 0);
+  auto load_row = [&](int k, float (&o)[kBtCh]) {
+    const int x = (k < n_int) ? (prog[2 * k] & 0xFFFF) : 0;
+#pragma unroll
+    for (int t = 0; t < kBtCh; ++t)
+      o[t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdp, voff[t], x * rowbytes, 0));
+  };
+  auto step = [&](int k, const float (&d)[kBtCh]) {
+    const int ex = prog[2 * k], ey = prog[2 * k + 1];
+    const int x = ex & 0xFFFF;
+    const int kind = (ex >> 16) & 0xF;
+    int out = 0;
+    if (kind != kBtUnreached) {
+      const bool sent = kind == kBtSentinel;
+      const bool root = kind == kBtRoot;
+      const int sp = root ? 0 : (int)sts[ey * SPW + sg];
+      const float* row = c + sp * Q + j0;
+      float bv = INFINITY;
+      int bi = j0;
+#pragma unroll
+      for (int t = 0; t < kBtCh; ++t) {
+        const bool ok = t < ch && j0 + t < Q;
+        const float dv = sent ? kSentinel : d[t];
+        const float v = ok ? (root ? dv : row[t] + dv) : INFINITY;
+        if (v < bv) { bv = v; bi = j0 + t; }
+      }
+      auto combine = [&](float ov, int oi) {
+        if (ov < bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      };
+      combine(__int_as_float(bt_partner<1>(__float_as_int(bv))), bt_partner<1>(bi));
+      combine(__int_as_float(bt_partner<2>(__float_as_int(bv))), bt_partner<2>(bi));
+      if constexpr (LPS == 8)
+        combine(__int_as_float(bt_partner<4>(__float_as_int(bv))), bt_partner<4>(bi));
+      out = bi;
+    }
+    if (q == 0) {
+      sts[x * SPW + sg] = (int8_t)out;
+      if (live) at[(size_t)x * L] = (int8_t)out;
+    }
+  };
+  float r0[kBtCh], r1[kBtCh], r2[kBtCh], r3[kBtCh];
+  load_row(0, r0);
+  load_row(1, r1);
+  load_row(2, r2);
+  load_row(3, r3);
+  for (int k = 0; k < n_int; k += 4) {
+    step(k, r0);
+    load_row(k + 4, r0);
+    if (k + 1 < n_int) step(k + 1, r1);
+    load_row(k + 5, r1);
+    if (k + 2 < n_int) step(k + 2, r2);
+    load_row(k + 6, r2);
+    if (k + 3 < n_int) step(k + 3, r3);
+    load_row(k + 7, r3);
+  }
+}
+
 template <int G, bool SOFT, bool RAGGED>
 void launch_wide(int phase, int grid, size_t lds, hipStream_t st, const WArgs& A) {
   if (phase == 1)
@@ -708,6 +813,24 @@ int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t st
 
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream) {
+  const char* e4 = std::getenv("TREX_BT4");  // A/B: 0 = one lane per site, 4 = four lanes
+  const int lps = (e4 && e4[0] == '4') ? 4 : 8;
+  if (Q <= 32 && !(e4 && e4[0] == '0') && (int64_t)ni * L * Q * 4 <= 0x7FFFFFF0LL &&
+      32 * 32 * 4 + (size_t)ni * (kWave / lps) <= 65536) {
+    const int spw = kWave / lps;
+    const int tiles4 = (L + spw - 1) / spw;
+    const size_t lds4 = 32 * 32 * 4 + (size_t)ni * spw;
+    if (lps == 8)
+      hipLaunchKernelGGL(wide_backtrack4_kernel<8>, dim3(B * tiles4), dim3(kWave), lds4,
+                         (hipStream_t)stream, bt, cost, dp, ni, L, Q, tiles4, anc);
+    else
+      hipLaunchKernelGGL(wide_backtrack4_kernel<4>, dim3(B * tiles4), dim3(kWave), lds4,
+                         (hipStream_t)stream, bt, cost, dp, ni, L, Q, tiles4, anc);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+      return set_error(TREX_E_HIP, "trex_sankoff_backtrack: %s", hipGetErrorString(e));
+    return TREX_OK;
+  }
   const int tiles = (L + kWave - 1) / kWave;
   const int mq = Q <= 32 ? 32 : 64;
   const size_t lds = (size_t)mq * mq * 4 + (size_t)ni * kWave;
