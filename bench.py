@@ -213,9 +213,20 @@ def c2_line(torch, device, args, cpu_threads):
     torch.cuda.synchronize()
     single_s = (time.perf_counter() - t0) / 500
     units = 10000 * 63 * 4
+    # trex-exact reconstruction of the same tree (run_sankoff(return_path=True)
+    # on the device: hard forward writing the DP table + backtrack)
+    rout = {"dp": torch.empty(eng.dp_shape, dtype=torch.float32, device=device),
+            "tree_score": torch.empty(1, device=device)}
+
+    def recon():
+        r = eng.forward(leaves, cost, 0.0, out=rout)
+        eng.backtrack(cost, r.dp)
+
+    recon_s = _replay_seconds(torch, recon, 200)
     out = {"workload": "C2: balanced 64-taxa tree x 10000 sites x 4 states, softmin tau=1.0 "
                        "fwd+grad, hipGraph of 10 steps replayed", "ms_per_step": gpu_s * 1e3,
-           "value": units / gpu_s, "ms_per_single_step_graph_replay": single_s * 1e3}
+           "value": units / gpu_s, "ms_per_single_step_graph_replay": single_s * 1e3,
+           "hard_recon_ms_per_step": recon_s * 1e3}
     from oracle.cpu_port import fwd_bwd
 
     fwd_bwd(ch, seqs[None, :64], cost.cpu().numpy(), 1.0, threads=cpu_threads)

@@ -104,9 +104,16 @@ def test_convergence_setup_invariant(device):
 # ---------------------------------------------------------------------------
 # run_sankoff == trex restatement, bit for bit
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("bt", ["split", "0"])
 @pytest.mark.parametrize("L", [1, 3, 64, 130, 1000, 4096])
 @pytest.mark.parametrize("Q", [2, 3, 4])
-def test_run_sankoff_bitexact_random_trees(device, L, Q):
+def test_run_sankoff_bitexact_random_trees(device, L, Q, bt, monkeypatch):
+    """bt: the backtrack on 4 lanes per site (default) or on the
+    sites-per-lane kernel (TREX_BT4=0)."""
+    if bt == "0":
+        monkeypatch.setenv("TREX_BT4", "0")
+    else:
+        monkeypatch.delenv("TREX_BT4", raising=False)
     ch = random_topologies(1, 16, seed=100 + L + Q)[0]
     adj = adjacency_from_children(ch)[0]
     rng = np.random.default_rng(L * 7 + Q)

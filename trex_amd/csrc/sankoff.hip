@@ -1522,7 +1522,11 @@ extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, con
   if (!plan || !cost || !dp || !anc_states)
     return set_error(TREX_E_ARG, "trex_sankoff_backtrack: null pointer argument");
   const int32_t* bt32 = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 4;
-  if (Q > 4) return wide_backtrack(bt32, cost, dp, B, L, s.ni, Q, anc_states, stream);
+  // split-lane kernel (wide_backtrack4_kernel, 4 lanes per site for Q <= 4);
+  // TREX_BT4=0 keeps the sites-per-lane kernel below (A/B, tested)
+  const char* e4 = std::getenv("TREX_BT4");
+  if (Q > 4 || !(e4 && e4[0] == '0'))
+    return wide_backtrack(bt32, cost, dp, B, L, s.ni, Q, anc_states, stream);
   const int spt = (L % 4 == 0) ? 4 : 1;
   const int tiles = tiles_for(L, spt);
   hipStream_t st = (hipStream_t)stream;
