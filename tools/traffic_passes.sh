@@ -6,6 +6,11 @@ set -e
 OUT=$(realpath -m "$1")
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$OUT"
+# calibration microbenchmarks (git-ignored binaries): build them if absent
+for m in load_pattern store_pattern; do
+  [ -x "$ROOT/tools/micro/$m" ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -w \
+    -o "$ROOT/tools/micro/$m" "$ROOT/tools/micro/$m.hip"
+done
 export TMPDIR=/tmp
 cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
