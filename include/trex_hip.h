@@ -48,6 +48,10 @@ extern "C" {
 #define TREX_PLAN_HEADER_INTS 16
 
 const char* trex_last_error(void);
+/* ABI / plan-layout version.  5: plans carry each tree's staged (multi-wave)
+ * program after the backtrack entries (trex_plan_ints grew; a binding that
+ * sized or cached v4 plans must re-query it), Q up to 64, ragged Q > 4.
+ * 4: site-major DP tables. */
 int trex_version(void);
 
 /* ------------------------------------------------------------------------

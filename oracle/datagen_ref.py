@@ -88,10 +88,60 @@ def _fixed_fitness(seq, inter, fit, Q):
     return int((vals * 2.0 ** 40).astype(np.int64).sum())
 
 
+def sorted_nodes_ref(adjacency):
+    """The traversal of trex's generate_tree_data, step by step as the JAX
+    program runs it (src/trex/nk_model.py:154-192).  Written independently of
+    trex_amd.datagen.reference_sorted_nodes so the two check each other.
+
+    Returns (root, parent, sorted_nodes) with the reference's -1 slots kept.
+    JAX semantics restated: jnp.argmax takes the first maximum (:154);
+    jnp.where(..., size=k) pads with 0 (:155, :170); ``x.at[i].set(v)`` with
+    i outside [0, n) is dropped (:167, :176); lax.cond reads ``visited``
+    as updated at :168.
+    """
+    A = np.asarray(adjacency)
+    n = A.shape[0]
+    parent = [int(np.argmax(A[r])) for r in range(n)]
+    selfp = [i for i in range(n) if parent[i] == i]
+    root = (selfp + [0])[0]
+    queue = [root] + [-1] * (n - 1)
+    visited = [False] * n
+    sorted_nodes = [-1] * n
+    guard = 0
+    while any(q != -1 for q in queue):
+        current = queue[0]
+        queue = queue[1:] + [-1]                    # .at[0].set(-1) then roll(-1)
+        slot = sum(visited)
+        if slot < n:
+            sorted_nodes[slot] = current
+        visited[current] = True
+        children = [i for i in range(n) if A[i, current] == 1]
+        children += [0] * (n - len(children))      # size=n, fill 0
+        for child in children:                     # fori_loop(0, n)
+            if not visited[child]:
+                pos = sum(q != -1 for q in queue)
+                if pos < n:
+                    queue[pos] = child
+        guard += 1
+        assert guard <= n * n + n, "BFS did not terminate"
+    return root, np.asarray(parent, np.int64), np.asarray(sorted_nodes, np.int64)
+
+
+def evolve_order_ref(adjacency):
+    """(root, parent, order) with the -1 slots resolved the way the evolve
+    loop indexes them (nk_model.py:199-262): ``sorted_nodes[i] = -1`` reads
+    ``parent_indices[-1]`` and writes ``sequences.at[-1]`` -- row n - 1 --
+    and ``-1 != root_node``, so the slot evolves even when n - 1 is the
+    root."""
+    root, parent, sn = sorted_nodes_ref(adjacency)
+    n = len(parent)
+    return root, parent, np.where(sn < 0, n - 1, sn)
+
+
 def generate_tree_data(seed, interactions, fitness, parent, order, root_seq, Q, mutation_rate,
                        noise_std, coupled_prob, branch_length):
     """trex_datagen_nk_tree restated (the device's draws and fixed-point
-    fitness): the nodes of ``order`` (trex_amd.datagen.bfs_levels: the
+    fitness): the nodes of ``order`` (``evolve_order_ref``: the
     reference's BFS sorted_nodes, root first, -1 slots resolved to the last
     node) evolve from their parents in slot order, slot s drawing from
     streams 4s .. 4s + 3 (nk_model.py:192-262); returns int8 (n_nodes, L)."""

@@ -92,9 +92,11 @@ def run_dp_ref(adj, dp, bt, seqs, cost, dtype=np.float32):
     n_leaves = (n_all + 1) // 2
     L, _, Q = dp.shape
     sites = np.arange(L)
-    # leaf init (sankoff.py:49-52): dp[i, int(seq[i])] = 0, negative wraps, OOB dropped
+    # leaf init (sankoff.py:49-52): dp[i, int(seq[i])] = 0, negative wraps, OOB dropped;
+    # int(.) is XLA's convert (_f2i: truncation, saturation, NaN -> 0), not numpy's astype
+    f2i = np.vectorize(_f2i, otypes=[np.int64])
     for i in range(n_leaves):
-        s = seqs[i].astype(np.int32)
+        s = f2i(seqs[i])
         s = np.where(s < 0, s + Q, s)
         ok = (s >= 0) & (s < Q)
         dp[sites[ok], i, s[ok]] = 0
@@ -231,10 +233,12 @@ def run_sankoff_ref(adj, cost, seqs, n_all, n_states, n_leaves, return_path=Fals
 def normalize_leaves(seqs: np.ndarray, n_states: int) -> np.ndarray:
     """trex leaf-state semantics as int8 codes: [0,Q) observed, -1 = all-1e5 row.
 
-    ``seq.astype(int32)`` truncates toward zero; negative states wrap once;
-    anything still out of range is dropped by the scatter (sankoff.py:50).
+    ``seq.astype(int32)`` is XLA's convert (truncation toward zero,
+    saturation, NaN -> 0, as ``_f2i``); negative states wrap once; anything
+    still out of range is dropped by the scatter (sankoff.py:50).
     """
     s = np.trunc(np.asarray(seqs, dtype=np.float64))
+    s = np.where(np.isnan(s), 0.0, s)
     s = np.where(s < 0, s + n_states, s)
     ok = (s >= 0) & (s < n_states)
     return np.where(ok, s, -1).astype(np.int8)

@@ -92,5 +92,42 @@ def weird_children(case):
     return ch
 
 
+def assert_grad_close(got, ref, rtol=1e-5, what="dC"):
+    """Elementwise gradient bar: |got - ref| <= rtol * |ref| for EVERY entry
+    (north_star: "grads within 1e-5 for the softmin relaxation").
+
+    No matrix-max atol: a softmin dC entry is a sum of non-negative terms
+    (softmax weight x cotangent), so each entry carries its own relative
+    error; a normwise bar would let the small entries drift.  The only
+    absolute slack is 1e-30, below fp32's normal range (1.2e-38) times the
+    ~1e8 terms an entry sums -- entries the fp64 oracle holds at < 1e-30 are
+    underflow in any fp32 arithmetic, the reference's included.  Returns the
+    max elementwise relative error (the message reports it on failure)."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    err = np.abs(got - ref)
+    bound = rtol * np.abs(ref) + 1e-30
+    rel = err / np.maximum(np.abs(ref), 1e-30)
+    bad = ~(err <= bound)
+    k = np.unravel_index(int(np.argmax(np.where(np.isfinite(rel), rel, np.inf))), rel.shape)
+    assert not bad.any(), (f"{what}: max elementwise rel err {rel[k]:.3e} at {k} "
+                           f"(got {got[k]!r}, ref {ref[k]!r}); {int(bad.sum())} of {bad.size} "
+                           f"entries above rtol {rtol:g}")
+    return float(rel[k])
+
+
+def offset_rtol(dp_ref, tau, rtol=1e-5):
+    """Per-entry relative bound when every D carries a large offset (a leaf
+    whose state is out of range keeps trex's all-1e5 row, sankoff.py:49-52,
+    152): an fp32 D value is rounded to half an ulp of |D|, and the softmin
+    weights depend on differences of two such values divided by tau, so each
+    weight -- hence each dC entry, a non-negative combination of them -- is
+    good to 2 * 2^-24 * max|D| / tau relative (the reference's own fp32
+    arithmetic has the same loss).  Never below rtol."""
+    return max(rtol, 2.0 * 2.0 ** -24 * float(np.abs(dp_ref).max()) / tau)
+
+
 __all__ = ["simulate_leaves", "hamming", "int_cost", "random_leaves", "balanced_children",
-           "weird_children", "random_topologies", "create_balanced_binary_tree"]
+           "weird_children", "random_topologies", "create_balanced_binary_tree",
+           "assert_grad_close", "offset_rtol"]

@@ -51,37 +51,52 @@ def test_uniform_states_device_c4_size(device):
     np.testing.assert_array_equal(tail, us_ref(4, x.numel(), 4, start=x.numel() - 4096))
 
 
-def _rooted_balanced(nl):
+def _adjacency(nl, kind):
+    """"root0": balanced tree relabelled so the self-parented root is node 0
+    (the reference's BFS then reaches every node); "last": root n - 1 with a
+    self-loop (the reference's 0-padded child lists overflow its queue, some
+    nodes are never evolved, the -1 slots re-evolve the root); "none": no
+    self-parented node (BFS rooted at node 0 by the jnp.where fill)."""
     from trex_amd.topology import create_balanced_binary_tree
 
     adj = create_balanced_binary_tree(nl).copy()
-    adj[-1, -1] = 1
+    n = adj.shape[0]
+    if kind == "root0":
+        perm = np.arange(n)
+        perm[[0, n - 1]] = [n - 1, 0]
+        adj = adj[np.ix_(perm, perm)]
+        adj[0, 0] = 1
+    elif kind == "last":
+        adj[-1, -1] = 1
     return adj
 
 
-@pytest.mark.parametrize("nl,L,Q,K,rate,std,cp,bl,rooted", [
-    (8, 64, 4, 2, 0.1, 0.0, 0.5, 1, True),
-    (16, 300, 4, 4, 0.05, 0.3, 0.5, 3, True),
-    (8, 50, 20, 2, 0.2, 0.0, 0.0, 2, True),
-    (4, 40, 2, 3, 0.1, 0.0, 1.0, 5, True),
-    (8, 64, 4, 2, 0.1, 0.0, 0.5, 1, False),   # the reference's -1 slot quirk
-    (32, 2000, 4, 4, 0.02, 0.5, 0.5, 2, True),
+@pytest.mark.parametrize("nl,L,Q,K,rate,std,cp,bl,kind", [
+    (8, 64, 4, 2, 0.1, 0.0, 0.5, 1, "root0"),
+    (16, 300, 4, 4, 0.05, 0.3, 0.5, 3, "root0"),
+    (8, 50, 20, 2, 0.2, 0.0, 0.0, 2, "root0"),
+    (4, 40, 2, 3, 0.1, 0.0, 1.0, 5, "root0"),
+    (8, 64, 4, 2, 0.1, 0.0, 0.5, 1, "none"),   # the reference's -1 slot quirk
+    (8, 64, 4, 2, 0.3, 0.0, 0.5, 2, "last"),   # queue overflow, root re-evolved
+    (32, 2000, 4, 4, 0.02, 0.5, 0.5, 2, "root0"),
 ])
-def test_nk_tree_device_matches_restatement(device, nl, L, Q, K, rate, std, cp, bl, rooted):
+def test_nk_tree_device_matches_restatement(device, nl, L, Q, K, rate, std, cp, bl, kind):
     """trex_datagen_nk_tree (generate_tree_data's process, nk_model.py:
     116-278) equals its CPU restatement bit for bit: same draws, fixed-point
-    fitness sums, BFS levels incl. the -1 tail."""
+    fitness sums, the reference's traversal (oracle.datagen_ref.
+    evolve_order_ref, independent of the device's level planner) incl. the
+    -1 tail and the dropped enqueues."""
+    from oracle.datagen_ref import evolve_order_ref
     from oracle.datagen_ref import generate_tree_data as nk_ref
-    from trex_amd.datagen import bfs_levels, create_nk_model_landscape, generate_tree_data_device
-    from trex_amd.topology import create_balanced_binary_tree
+    from trex_amd.datagen import create_nk_model_landscape, generate_tree_data_device
 
     ls = create_nk_model_landscape(L, K, seed=nl + L, n_states=Q)
-    adj = _rooted_balanced(nl) if rooted else create_balanced_binary_tree(nl)
+    adj = _adjacency(nl, kind)
     rs = np.random.default_rng(L).integers(0, Q, L)
     got = generate_tree_data_device(ls, adj, rs, rate, seed=21, coupled_mutation_prob=cp,
                                     mutation_rate_noise_std=std, branch_length=bl,
                                     device=device).cpu().numpy()
-    _, parent, order, _ = bfs_levels(adj)
+    _, parent, order = evolve_order_ref(adj)
     ref = nk_ref(21, ls["interactions"], ls["fitness_tables"], parent, order, rs, Q, rate, std, cp,
                  bl)
     np.testing.assert_array_equal(got, ref)

@@ -83,7 +83,11 @@ def test_c4_tree_sharding_world2_on_one_gpu():
     mp.spawn(_c4_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for r in range(world):
         gdc, gloss, dc_full, loss_full = out[r]
-        np.testing.assert_allclose(gdc, dc_full, rtol=1e-6, atol=1e-6 * np.abs(dc_full).max())
+        # the shards' fp64 partials are summed in a different association
+        # than the single-process reduce: elementwise to fp32 rounding
+        from _cases import assert_grad_close
+
+        assert_grad_close(gdc, dc_full, rtol=1e-6)
         np.testing.assert_allclose(gloss, loss_full, rtol=1e-6)
     assert np.array_equal(out[0][0], out[1][0])
 

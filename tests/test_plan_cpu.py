@@ -223,3 +223,10 @@ def test_plan_rejects_bad_children():
 def test_adjacency_roundtrip():
     ch = random_topologies(3, 12, seed=5)
     np.testing.assert_array_equal(children_from_adjacency(adjacency_from_children(ch)), ch)
+
+
+def test_abi_version_matches_plan_layout():
+    """trex_version() 5: plans carry the staged program of every tree after
+    the backtrack entries (include/trex_hip.h); a binding that sized v4
+    plans itself must see the bump."""
+    assert lib().trex_version() == 5

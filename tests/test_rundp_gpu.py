@@ -91,7 +91,8 @@ def test_vectorized_dp_matches_restatement(device, Q, init, topo):
     L = 300
     dp0, bt0 = _random_tables(rng, L, n_all, Q, init=init)
     seqs = rng.integers(-Q, Q + 2, size=((n_all + 1) // 2 + 1, L)).astype(np.float32)
-    seqs[0, :5] = [0.7, -0.2, np.nan, 1e12, -1.5]  # truncation, wrap, dropped
+    # truncation, wrap, NaN -> state 0 (XLA's convert), saturated -> dropped
+    seqs[0, :5] = [0.7, -0.2, np.nan, 1e12, -1.5]
     cost = int_cost(Q, seed=Q).astype(np.float32)
     with np.errstate(invalid="ignore"):
         r_dp, r_bt = run_dp_ref(adj, dp0, bt0, seqs, cost)

@@ -58,6 +58,26 @@ int rccl_fail(const char* fn, const Rccl* r, ncclResult_t e) {
 
 using namespace trex;
 
+// Switches the calling thread's current device for the duration of a call
+// and restores the caller's on every return path (a process may drive
+// several GPUs: torch, or a C caller).
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int dev) {
+    ok_ = hipGetDevice(&prev_) == hipSuccess && hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  bool ok() const { return ok_; }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+ private:
+  int prev_ = -1;
+  bool ok_ = false;
+};
+
 extern "C" int trex_comm_unique_id_bytes(void) { return NCCL_UNIQUE_ID_BYTES; }
 
 extern "C" int trex_comm_get_unique_id(void* id) {
@@ -76,7 +96,8 @@ extern "C" int trex_comm_init(void** comm, int nranks, const void* id, int rank,
   if (!r) return set_error(TREX_E_UNSUPPORTED, "%s: RCCL not loadable", fn);
   if (!comm || !id || nranks < 1 || rank < 0 || rank >= nranks || dev < 0)
     return set_error(TREX_E_ARG, "%s: bad arguments", fn);
-  if (hipSetDevice(dev) != hipSuccess) return set_error(TREX_E_HIP, "%s: hipSetDevice(%d)", fn, dev);
+  DeviceGuard guard(dev);
+  if (!guard.ok()) return set_error(TREX_E_HIP, "%s: hipSetDevice(%d)", fn, dev);
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
   ncclComm_t c = nullptr;
@@ -100,7 +121,8 @@ extern "C" int trex_allreduce_sum(float* buf, int count, int dev, void* comm, vo
   if (!r) return set_error(TREX_E_UNSUPPORTED, "%s: RCCL not loadable", fn);
   if (!buf || count < 0 || !comm || dev < 0) return set_error(TREX_E_ARG, "%s: bad arguments", fn);
   if (count == 0) return TREX_OK;
-  if (hipSetDevice(dev) != hipSuccess) return set_error(TREX_E_HIP, "%s: hipSetDevice(%d)", fn, dev);
+  DeviceGuard guard(dev);
+  if (!guard.ok()) return set_error(TREX_E_HIP, "%s: hipSetDevice(%d)", fn, dev);
   if (ncclResult_t e = r->all_reduce(buf, buf, (size_t)count, ncclFloat32, ncclSum,
                                      static_cast<ncclComm_t>(comm), (hipStream_t)stream))
     return rccl_fail(fn, r, e);

@@ -59,9 +59,11 @@ struct MinArg {
   int j;
 };
 
-// trex leaf code: int32 truncation, negative wraps once, -1 = dropped
+// trex leaf code: XLA's f32 -> s32 convert (truncation, saturation, NaN -> 0),
+// negative wraps once, -1 = dropped
 __device__ __forceinline__ int leaf_state(float x, int Q) {
-  if (!(x > -2147483648.0f && x < 2147483648.0f)) return -1;  // NaN / huge: dropped
+  if (is_nan(x)) return 0;
+  if (!(x > -2147483648.0f && x < 2147483648.0f)) return -1;  // saturated: out of range, dropped
   int s = (int)x;  // truncation toward zero
   if (s < 0) s += Q;
   return (s >= 0 && s < Q) ? s : -1;

@@ -1453,7 +1453,7 @@ using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 4; }
+extern "C" int trex_version(void) { return 5; }
 
 extern "C" int trex_dp_site_major(int Q) {
   (void)Q;

@@ -11,9 +11,10 @@ JAX's threefry PRNG, which cannot run here; ``seed`` seeds numpy's PCG64):
 * ``get_fitness``          src/trex/nk_model.py:46-110
 * ``generate_tree_data``   src/trex/nk_model.py:116-278, including its index
   semantics: the root is the first node whose argmax parent is itself
-  (``jnp.where(..., size=1)`` fills 0 when there is none), BFS order from it,
-  and unfilled BFS slots are -1, which index the LAST node (numpy/JAX
-  negative-index wrap), as in the reference.
+  (``jnp.where(..., size=1)`` fills 0 when there is none), the reference's
+  fixed-size BFS queue with 0-padded child lists and dropped out-of-range
+  writes (``reference_sorted_nodes``), and unfilled BFS slots are -1, which
+  index the LAST node (numpy/JAX negative-index wrap), as in the reference.
 
 Outputs are numpy arrays in the reference's dtypes/shapes; move them to the
 device with torch when a kernel needs them.
@@ -94,25 +95,55 @@ def get_fitness(sequence, landscape: dict, seq_mask=None) -> float:
     return float((vals * mask).sum() / mask.sum())
 
 
-def _bfs_order(adjacency, parent):
-    n = adjacency.shape[0]
+def reference_sorted_nodes(adjacency):
+    """generate_tree_data's traversal, restated with JAX's semantics
+    (nk_model.py:154-192).  Returns (root, parent, sorted_nodes int64 (n,)).
+
+    * parent = first argmax of each adjacency row (:154); root = the first
+      node that is its own parent, 0 when none is (``jnp.where(size=1)``'s
+      fill value, :155);
+    * a fixed queue of n slots, -1 = empty (:184); each step pops slot 0 and
+      rolls (:163-165), writes the popped node to
+      ``sorted_nodes[sum(visited)]`` BEFORE marking it (:167-168) -- so a
+      node popped twice overwrites the slot the next new node then takes,
+      and a write at index n is dropped (JAX scatter out of bounds);
+    * children = ``jnp.where(adj[:, node] == 1, size=n)`` padded with 0
+      (:170), each enqueued at ``sum(queue != -1)`` if not yet visited
+      (:172-181) -- the pads enqueue node 0 over and over while it is
+      unvisited, and enqueues past the last slot are dropped, so some nodes
+      may never be reached (their rows stay zero in the reference);
+    * unfilled slots stay -1 (:186), which the evolve loop indexes as the
+      last node (:199-262).
+    """
+    A = np.asarray(adjacency)
+    n = A.shape[0]
+    parent = np.argmax(A, axis=1).astype(np.int64)
     selfp = np.nonzero(parent == np.arange(n))[0]
-    root = int(selfp[0]) if selfp.size else 0  # jnp.where(size=1) fill value 0
-    order = np.full(n, -1, dtype=np.int64)
+    root = int(selfp[0]) if selfp.size else 0
+    queue = np.full(n, -1, np.int64)
+    queue[0] = root
     visited = np.zeros(n, bool)
-    queue = [root]
-    t = 0
-    while queue:
-        node = queue.pop(0)
-        order[int(visited.sum())] = node
-        visited[node] = True
-        for c in np.nonzero(adjacency[:, node] == 1)[0]:
+    order = np.full(n, -1, np.int64)
+    steps = 0
+    while (queue != -1).any():
+        cur = int(queue[0])
+        queue[0] = -1
+        queue = np.roll(queue, -1)
+        k = int(visited.sum())
+        if k < n:
+            order[k] = cur
+        visited[cur] = True
+        kids = np.nonzero(A[:, cur] == 1)[0]
+        kids = np.concatenate([kids, np.zeros(n - kids.size, np.int64)])
+        for c in kids:
             if not visited[c]:
-                queue.append(int(c))
-        t += 1
-        if t > n:
-            break
-    return root, order
+                pos = int((queue != -1).sum())
+                if pos < n:
+                    queue[pos] = c
+        steps += 1
+        if steps > n * n + n:  # every pop either visits a node or drains a duplicate
+            raise RuntimeError("reference_sorted_nodes: BFS did not terminate")
+    return root, parent, order
 
 
 def generate_tree_data(landscape: dict, adjacency, root_sequence, mutation_rate: float, seed=0,
@@ -128,14 +159,13 @@ def generate_tree_data(landscape: dict, adjacency, root_sequence, mutation_rate:
     L = root_seq.shape[0]
     if "n_states" in landscape:
         n_states = int(landscape["n_states"])
-    parent = np.argmax(A, axis=1)
-    root, order = _bfs_order(A, parent)
+    root, parent, order = reference_sorted_nodes(A)
     seqs = np.zeros((n, L), dtype=np.int64)
     seqs[root] = root_seq
     inter = np.asarray(landscape["interactions"])
     for i in range(n):
         node = int(order[i])  # -1 wraps to the last node, as in the reference
-        if node == root:
+        if node == root:  # -1 != root_node (:257): a -1 slot evolves row n-1 even if it is the root
             continue
         rate = min(mutation_rate * np.exp(rng.normal() * mutation_rate_noise_std), 1.0)
         seq = seqs[parent[node]].copy()
@@ -204,37 +234,30 @@ def uniform_states_device(shape, n_states: int, seed: int = 0, device="cuda"):
 
 
 def bfs_levels(adjacency):
-    """generate_tree_data's traversal (nk_model.py:149-190) as launch levels:
-    parent = argmax of each adjacency row, root = the first self-parented
-    node (0 when there is none, the jnp.where fill), BFS from it.  Returns
-    (root, parent, order, offsets): ``order`` is the reference's
-    sorted_nodes with its unfilled -1 slots resolved as the reference's
-    indexing does (the last node), ``offsets`` the launch levels -- BFS
-    levels for the reached nodes, then one slot per level for the -1 tail
-    (each re-evolves the last node from its parent, in sequence)."""
-    A = np.asarray(adjacency)
-    n = A.shape[0]
-    parent = np.argmax(A, axis=1).astype(np.int32)
-    roots = np.nonzero(parent == np.arange(n))[0]
-    root = int(roots[0]) if roots.size else 0
-    order, offsets, frontier, seen = [], [0], [root], {root}
-    while frontier:
-        order.extend(frontier)
-        offsets.append(len(order))
-        nxt = []
-        for node in frontier:
-            for c in np.nonzero(A[:, node] == 1)[0]:
-                c = int(c)
-                if c not in seen:
-                    seen.add(c)
-                    nxt.append(c)
-        frontier = nxt
-    # -1 slots index node n - 1; the reference leaves it alone when it is the
-    # root (node_index == root_node), otherwise re-evolves it once per slot
-    while len(order) < n and root != n - 1:
-        order.append(n - 1)
-        offsets.append(len(order))
-    return root, parent, np.asarray(order, np.int32), np.asarray(offsets, np.int32)
+    """generate_tree_data's evolve order (nk_model.py:194-269) as launch
+    levels for the device.  Returns (root, parent, order, offsets):
+    ``order`` is the reference's sorted_nodes (``reference_sorted_nodes``)
+    with its -1 slots resolved as the reference indexes them (node n - 1,
+    evolved from parent[n - 1] even when that is the root), slot 0 the root
+    (never evolved); ``offsets`` cut the slots into levels a launch may run
+    in parallel: consecutive slots none of which writes a row another slot
+    of the level reads or writes.  Sequential slot order is the semantics;
+    levels only batch slots whose order does not matter."""
+    root, parent, sorted_nodes = reference_sorted_nodes(adjacency)
+    n = parent.shape[0]
+    order = np.where(sorted_nodes < 0, n - 1, sorted_nodes).astype(np.int32)
+    offsets = [0, 1]
+    written, read = set(), set()
+    for slot in range(1, n):
+        node, par = int(order[slot]), int(parent[order[slot]])
+        if node in written or node in read or par in written:
+            offsets.append(slot)
+            written, read = set(), set()
+        written.add(node)
+        read.add(par)
+    if offsets[-1] != n:
+        offsets.append(n)
+    return root, parent.astype(np.int32), order, np.asarray(offsets, np.int32)
 
 
 def generate_tree_data_device(landscape: dict, adjacency, root_sequence, mutation_rate: float,
@@ -257,6 +280,16 @@ def generate_tree_data_device(landscape: dict, adjacency, root_sequence, mutatio
     L = int(np.asarray(root_sequence).reshape(-1).shape[0])
     K = int(inter.shape[1]) if inter.ndim == 2 else 0
     n = parent.shape[0]
+    # the kernel indexes LDS and the fitness table with these: validate here
+    # (the reference's jnp gathers would clamp; out-of-range input is a bug)
+    rs_host = np.asarray(root_sequence).reshape(-1)
+    if inter.size and (inter.shape[0] != L or inter.min() < 0 or inter.max() >= L):
+        raise ValueError(f"interactions must be (L={L}, K) with entries in [0, {L})")
+    if rs_host.size and (rs_host.min() < 0 or rs_host.max() >= n_states):
+        raise ValueError(f"root_sequence states must lie in [0, {n_states})")
+    if fit.shape != (L, n_states ** (K + 1)):
+        raise ValueError(f"fitness_tables must be (L, Q^(K+1)) = ({L}, {n_states ** (K + 1)}), "
+                         f"got {fit.shape}")
     seqs = torch.zeros((n, L), dtype=torch.int8, device=dev)
     seqs[root] = torch.as_tensor(np.asarray(root_sequence).reshape(-1).astype(np.int8), device=dev)
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731

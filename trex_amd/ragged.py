@@ -256,6 +256,7 @@ def from_padded(adjacency, node_mask, sequences, seq_mask, n_states: int):
         children.append(children_from_adjacency(A[b, :n_all, :n_all])[0])
         Ls.append(L)
         s = np.trunc(S[b, :nl, :L].astype(np.float64))
+        s = np.where(np.isnan(s), 0.0, s)  # XLA's f32 -> s32 convert: NaN -> 0
         s = np.where(s < 0, s + n_states, s)
         leaves.append(np.where((s >= 0) & (s < n_states), s, -1).astype(np.int8))
         shapes.append((n_all, L))

@@ -39,14 +39,16 @@ def _default_device():
 def leaf_codes(sequences, n_states: int, device=None):
     """trex leaf states -> int8 codes on the device.
 
-    ``seq.astype(int32)`` truncates toward zero, negative states wrap once,
-    anything else out of range is a dropped scatter (all-1e5 row,
-    sankoff.py:49-52); such leaves get code -1.
+    ``seq.astype(int32)`` is XLA's convert: truncation toward zero,
+    saturation, NaN -> 0; negative states wrap once, anything else out of
+    range is a dropped scatter (all-1e5 row, sankoff.py:49-52); such leaves
+    get code -1.
     """
     torch = _torch()
     device = device or _default_device()
     s = torch.as_tensor(sequences).to(device=device, dtype=torch.float64)
     s = torch.trunc(s)
+    s = torch.where(torch.isnan(s), torch.zeros_like(s), s)
     s = torch.where(s < 0, s + n_states, s)
     ok = (s >= 0) & (s < n_states)
     return torch.where(ok, s, torch.full_like(s, -1)).to(torch.int8).contiguous()
