@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-nk", action="store_true", help="skip the NK landscape-aware line")
     ap.add_argument("--no-ragged", action="store_true", help="skip the ragged-batch line")
     ap.add_argument("--no-shard", action="store_true", help="skip the 128-tree shard line")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the H2D-inclusive C4 line")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/pmc_traffic.py)")
@@ -163,6 +164,36 @@ def shard_line(torch, device, ch, leaves, cost, tau, L, Q, n, Bs):
             "ms_per_step": sec * 1e3, "value": Bs * L * (n - 1) * Q / sec,
             "fused_kernel_us": round(kt * 1e6, 2), "algorithmic_bytes": fb,
             "hbm_frac": round(fb / kt / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def e2e_line(torch, run_step, leaves, units, reps=10):
+    """C4 end to end (SURVEY 8(d) "kernel-only and end-to-end incl. H2D of
+    leaves"): each step first uploads the int8 leaves from host memory into
+    the device buffer the step reads, then runs the fused fwd + grad --
+    from pageable memory (a plain numpy array) and from pinned memory."""
+    host = leaves.cpu()
+    pinned = host.pin_memory()
+    nbytes = leaves.numel() * leaves.element_size()
+    out = {"workload": "C4 as the headline line, leaves uploaded from host memory every step",
+           "leaf_bytes": nbytes}
+    for name, src in (("pageable", host), ("pinned", pinned)):
+        leaves.copy_(src, non_blocking=True)
+        run_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            leaves.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        h2d = (time.perf_counter() - t0) / reps
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            leaves.copy_(src, non_blocking=True)
+            run_step()
+        torch.cuda.synchronize()
+        sec = (time.perf_counter() - t0) / reps
+        out[name] = {"ms_per_step_incl_h2d": sec * 1e3, "h2d_ms": h2d * 1e3,
+                     "h2d_GBs": round(nbytes / h2d / 1e9, 1), "value": units / sec}
+    return out
 
 
 def c2_line(torch, device, args, cpu_threads):
@@ -662,6 +693,17 @@ def main():
     n_int = n - 1
     units = args.trees * L * n_int * Q  # the whole batch, all ranks
     value = units * args.steps / el
+    dump = os.environ.get("TREX_BENCH_DUMP")
+    if dump and rank == 0:
+        # the last step's reduced [dC (Q*Q), loss] (rank 0's copy after the
+        # all-reduce; at N = 1 the step's own dC and loss): tests compare it
+        # with the single-process engine over the whole batch
+        if world > 1:
+            last = reds[(it[0] - 1) % 2]
+        else:
+            last = torch.cat([step.out_b["d_cost"].view(-1),
+                              step.out_f["tree_score"].sum().view(1)])
+        np.save(dump, last.cpu().numpy())
 
     # per-kernel device time (HIP events) -> roofline of the step's kernel
     kt = time_kernels(torch, step)
@@ -726,6 +768,8 @@ def main():
             result["cpu_baseline"] = cpu_baseline(ch, leaves.cpu().numpy(), cost.cpu().numpy(),
                                                   tau, L, n, Q, threads)
             result["cpu_baseline"]["host"] = hinfo
+        if not args.no_e2e:
+            result["c4_e2e"] = e2e_line(torch, run_once, leaves, units)
         if not args.no_shard:
             result["c4_shard"] = shard_line(torch, device, ch, leaves, cost, tau, L, Q, n,
                                             min(128, B))

@@ -244,6 +244,12 @@ int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
  * tree.py:127 rewrites only the ancestor rows). */
 int trex_tree_gram_skip(const float* S, int N, int64_t K, int skip_rows, float* G,
                         void* workspace, int64_t workspace_bytes, void* stream);
+/* Site-sharded optimisation with the cached leaf block: each rank's skip
+ * Gram covers rows [row0, N) x all columns (row0 = floor(skip_rows/64)*64);
+ * the ranks all-reduce those rows only (contiguous, row-major), then
+ * G[i][j] = G[j][i] for i < row0 <= j restores the leaf rows' ancestor
+ * columns from the reduced values (trex_amd.tree.TreeOptimizer(group=...)). */
+int trex_tree_gram_mirror(float* G, int N, int row0, void* stream);
 int trex_tree_surrogate_combine(const float* A, const float* G, int N, float* loss, float* dA,
                                 float* M, void* workspace, void* stream);
 int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS, void* stream);
@@ -259,7 +265,8 @@ int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t K, int row0
  * the same 1e-5 relative bar vs fp64 (tests/test_tree_gpu.py).  Contract:
  * every |operand| <= its max_abs (the optimisation loop's S is a softmax /
  * one-hot, max 1; M = diag(r+c) - (A+A^T) with softmax rows of A, max N+1);
- * a larger value overflows f16 (inf).  K % 16 == 0 for the Gram. */
+ * a larger value overflows f16 (inf).  K % 4 == 0 (16-B aligned rows; a
+ * ragged last 16- / 32-column block is masked), else TREX_E_UNSUPPORTED. */
 int trex_tree_gram_skip_x3(const float* S, int N, int64_t K, int skip_rows, float max_abs,
                            float* G, void* workspace, int64_t workspace_bytes, void* stream);
 int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64_t K, int row0, int nrows,

@@ -117,17 +117,22 @@ def assert_grad_close(got, ref, rtol=1e-5, what="dC"):
     return float(rel[k])
 
 
-def offset_rtol(dp_ref, tau, rtol=1e-5):
-    """Per-entry relative bound when every D carries a large offset (a leaf
-    whose state is out of range keeps trex's all-1e5 row, sankoff.py:49-52,
-    152): an fp32 D value is rounded to half an ulp of |D|, and the softmin
-    weights depend on differences of two such values divided by tau, so each
-    weight -- hence each dC entry, a non-negative combination of them -- is
-    good to 2 * 2^-24 * max|D| / tau relative (the reference's own fp32
-    arithmetic has the same loss).  Never below rtol."""
+def cond_rtol(dp_ref, tau, rtol=1e-5):
+    """Per-entry relative bound set by fp32 D itself, for the cases where it
+    exceeds 1e-5: the DP table is fp32 (as trex returns it), so each D value
+    is rounded to half an ulp of |D|; a softmin weight
+    w = exp((M_c[i] - C_ij - D_c[j]) / tau) has relative error equal to the
+    absolute error of its exponent, ~ 2 * 2^-24 * max|D| / tau (the errors
+    of the two D-like terms; normalisation keeps the dominant weights far
+    more accurate, the tiny ones -- e^-40-class at tau = 0.05 -- carry the
+    full amount).  Each dC entry is a non-negative combination of such
+    weights, so this bounds it elementwise.  Used where the bound exceeds
+    1e-5: leaves with out-of-range states (trex's all-1e5 row,
+    sankoff.py:49-52,152, puts a 1e5 offset into every D) and tau = 0.05
+    with costs up to 9 (|D| / tau ~ 2 000).  Never below rtol."""
     return max(rtol, 2.0 * 2.0 ** -24 * float(np.abs(dp_ref).max()) / tau)
 
 
 __all__ = ["simulate_leaves", "hamming", "int_cost", "random_leaves", "balanced_children",
            "weird_children", "random_topologies", "create_balanced_binary_tree",
-           "assert_grad_close", "offset_rtol"]
+           "assert_grad_close", "cond_rtol"]

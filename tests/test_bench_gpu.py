@@ -1,0 +1,78 @@
+"""bench.py's N > 1 path, rehearsed on one MI355X.
+
+The driver runs ``torch.distributed.run --nproc-per-node N bench.py --gpus N``
+on an 8-GPU node with RCCL; this box has one GPU, so the same command runs
+with TREX_BENCH_DEVICE_SHARE=1 (both ranks on cuda:0, gloo instead of RCCL:
+the code path, not the timing).  Checked:
+
+* rc 0 and one JSON line from rank 0;
+* ``value`` counts the WHOLE batch (every tree of every rank) per step;
+* the all-reduced [dC, loss] rank 0 holds after the last step equals the
+  single-process engine over the whole batch (the shards' sum).
+
+Fresh child processes via torch.distributed.run; the parent only touches
+the GPU after they have exited.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from _cases import assert_grad_close
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_bench_world2_device_share_sums_the_whole_batch(tmp_path):
+    trees, taxa, sites, states, steps = 64, 32, 1000, 4, 3
+    dump = tmp_path / "reduced.npy"
+    env = dict(os.environ, TREX_BENCH_DEVICE_SHARE="1", TREX_BENCH_DUMP=str(dump))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--steps", str(steps), "--warmup", "1", "--trees", str(trees),
+           "--taxa", str(taxa), "--sites", str(sites), "--states", str(states), "--no-c5"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["trees"] == trees
+    assert res["config"]["trees_rank0"] == trees // 2
+    units = trees * sites * (taxa - 1) * states
+    np.testing.assert_allclose(res["value"], units / (res["ms_per_step"] * 1e-3), rtol=1e-9)
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    from trex_amd import SankoffEngine
+
+    dev = torch.device("cuda", 0)
+    ch, plan, leaves, cost = bench.make_inputs(torch, dev, trees, taxa, sites, states, 0, trees)
+    eng = SankoffEngine(plan, sites, states, dev)
+    f, dc, _, _ = eng.fwd_bwd(leaves, cost, 0.5)
+    torch.cuda.synchronize()
+    red = np.load(dump)
+    q2 = states * states
+    # two shards' fp64-reduced dC partials summed in fp32: elementwise to
+    # fp32 rounding of the sum
+    assert_grad_close(red[:q2].reshape(states, states), dc.cpu().numpy(), rtol=1e-6)
+    np.testing.assert_allclose(red[q2], float(f.tree_score.double().sum()), rtol=1e-6)

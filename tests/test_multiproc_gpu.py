@@ -103,12 +103,12 @@ def _c5_case(nl=32, L=512, Q=4, seed=3):
     return S, params, noise
 
 
-def _c5_worker(rank, world, port, clip, out):
+def _c5_worker(rank, world, port, clip, L, out):
     dev = _init(rank, world, port)
     from trex_amd.distributed import shard_bounds
     from trex_amd.tree import TreeOptimizer
 
-    S, params, noise = _c5_case()
+    S, params, noise = _c5_case(L=L)
     L = S.shape[1]
     lo, hi = shard_bounds(L, rank, world)
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
@@ -117,6 +117,8 @@ def _c5_worker(rank, world, port, clip, out):
     shard = TreeOptimizer(t(S[:, lo:hi]), {"tree_params": t(params["tree_params"]),
                                            "ancestors": t(params["ancestors"][:, lo:hi])},
                           lr=0.01, clip_norm=clip, group=dist.group.WORLD)
+    # the split-product GEMMs on every shard, ragged K included (no silent f32)
+    assert single.gemm == "x3" and shard.gemm == "x3", (single.gemm, shard.gemm)
     temps = [2.0, 1.5, 1.2, 1.0]
     l1, l2 = [], []
     for i, T_ in enumerate(temps):
@@ -133,11 +135,15 @@ def _c5_worker(rank, world, port, clip, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("clip", [None, 1.0])
-def test_c5_site_sharding_world2_on_one_gpu(clip):
+@pytest.mark.parametrize("clip,L", [(None, 512), (1.0, 512), (None, 510)])
+def test_c5_site_sharding_world2_on_one_gpu(clip, L):
+    """L = 510: each rank holds 255 sites, K = 1 020 (K % 16 = 12, like the
+    C5 shard at N = 8, K = 25 000): the x3 GEMMs run on the ragged K and the
+    cached leaf x leaf Gram survives sharding (only the ancestor rows are
+    all-reduced per step, then mirrored)."""
     world = 2
     out = mp.Manager().dict()
-    mp.spawn(_c5_worker, args=(world, _free_port(), clip, out), nprocs=world, join=True)
+    mp.spawn(_c5_worker, args=(world, _free_port(), clip, L, out), nprocs=world, join=True)
     for r in range(world):
         l1, l2, tp1, tp2, an1, an2 = out[r]
         np.testing.assert_allclose(l2, l1, rtol=1e-5)

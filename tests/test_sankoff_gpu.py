@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_grad_close, balanced_children, hamming, int_cost, offset_rtol,
+from _cases import (assert_grad_close, balanced_children, cond_rtol, hamming, int_cost,
                     random_leaves, random_topologies, simulate_leaves, weird_children)
 from oracle.sankoff_ref import normalize_leaves, run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref
@@ -26,14 +26,15 @@ pytestmark = pytest.mark.gpu
 SOFT_RTOL = 1e-5
 
 
-@pytest.fixture(autouse=True, params=["lane-per-site", "state-parallel", "staged", "auto"])
+@pytest.fixture(autouse=True, params=["lane-per-site", "state-parallel", "staged"])
 def q4_kernel(request, monkeypatch):
-    """Every Q <= 4 case runs four times: on the lane-per-site kernel (the
-    C4 headline path), on the state-parallel kernel (4 lanes per site, one
-    DPP quad, G = 4; Q = 2 / 3 pad the quad), on the staged kernel (the
-    state-parallel item as a workgroup of waves over the tree's levels,
-    sankoff_staged.hip) and under the library's policy (sankoff.hip
-    wide_small_q / use_staged: small grids go staged)."""
+    """Every Q <= 4 case runs once on each of the three live kernels the
+    policy (sankoff.hip wide_small_q / use_staged) chooses between: the
+    lane-per-site kernel (the C4 headline path), the state-parallel kernel
+    (4 lanes per site, one DPP quad, G = 4; Q = 2 / 3 pad the quad) and the
+    staged kernel (the state-parallel item as a workgroup of waves over the
+    tree's levels, sankoff_staged.hip).  The policy itself runs in
+    tests/test_configs_full_gpu.py and tests/test_rundp_gpu.py."""
     if request.param == "lane-per-site":
         monkeypatch.setenv("TREX_WIDE_SMALLQ", "0")
     elif request.param == "state-parallel":
@@ -104,16 +105,11 @@ def test_convergence_setup_invariant(device):
 # ---------------------------------------------------------------------------
 # run_sankoff == trex restatement, bit for bit
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("bt", ["split", "0"])
 @pytest.mark.parametrize("L", [1, 3, 64, 130, 1000, 4096])
 @pytest.mark.parametrize("Q", [2, 3, 4])
-def test_run_sankoff_bitexact_random_trees(device, L, Q, bt, monkeypatch):
-    """bt: the backtrack on 4 lanes per site (default) or on the
-    sites-per-lane kernel (TREX_BT4=0)."""
-    if bt == "0":
-        monkeypatch.setenv("TREX_BT4", "0")
-    else:
-        monkeypatch.delenv("TREX_BT4", raising=False)
+def test_run_sankoff_bitexact_random_trees(device, L, Q):
+    """The backtrack runs on the split-lane kernel (4 lanes per site); its
+    one-lane-per-site twin is forced in tests/test_sankoff_wide_gpu.py."""
     ch = random_topologies(1, 16, seed=100 + L + Q)[0]
     adj = adjacency_from_children(ch)[0]
     rng = np.random.default_rng(L * 7 + Q)
@@ -261,7 +257,7 @@ def test_softmin_missing_leaves_fp32_offset(device):
     f = eng.forward(lv, c, tau)
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     dc, _, _ = eng.backward(lv, c, tau, f.dp)
-    assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=offset_rtol(ref["dp"], tau))
+    assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=cond_rtol(ref["dp"], tau))
 
 
 def test_softmin_direct_path_large_cost_over_tau(device):

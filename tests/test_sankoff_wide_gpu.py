@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_grad_close, hamming, int_cost, offset_rtol, random_leaves,
+from _cases import (assert_grad_close, cond_rtol, hamming, int_cost, random_leaves,
                     random_topologies)
 from oracle.sankoff_ref import run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref
@@ -98,14 +98,18 @@ def test_batched_hard_fwd_grad_wide(device, L, Q, n):
     np.testing.assert_allclose(_sm(mg), ref["marginals"], rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("bt", ["8", "4", "0"])
+@pytest.mark.parametrize("bt", ["split", "0"])
 @pytest.mark.parametrize("Q,ties", [(20, False), (20, True), (7, False), (5, True), (32, True),
                                     (61, False)])
 def test_backtrack_wide_matches_reference(device, Q, ties, bt, monkeypatch):
-    """trex-exact states on every Q > 4 backtrack kernel: 8 or 4 lanes per
-    site (Q <= 32, TREX_BT4) and one lane per site; Hamming costs (ties:
-    the first-index argmin rule across the lanes' state ranges)."""
-    monkeypatch.setenv("TREX_BT4", bt)
+    """trex-exact states on both live backtrack kernels: 8 lanes per site
+    (Q <= 32, the policy) and one lane per site (codons, ragged, forced here
+    by TREX_BT4=0); Hamming costs (ties: the first-index argmin rule across
+    the lanes' state ranges)."""
+    if bt == "0":
+        monkeypatch.setenv("TREX_BT4", "0")
+    else:
+        monkeypatch.delenv("TREX_BT4", raising=False)
     B, n, L = 3, 24, 515
     ch = random_topologies(B, n, seed=3 + Q)
     leaves = random_leaves(B, n, L, Q, seed=4 + Q)
@@ -164,7 +168,9 @@ def test_softmin_wide_direct_path_and_hard_root(device):
         np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"],
                                    rtol=SOFT_RTOL)
         dc, _, _ = eng.backward(lv, c, tau, f.dp, hard_root=hard_root)
-        assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
+        # tau = 0.05 with costs up to 9: tiny weights (e^-40) carry the fp32
+        # D conditioning |D| / tau (measured 4.6e-5 on 20 of 400 entries)
+        assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=cond_rtol(ref["dp"], tau))
 
 
 def test_softmin_wide_missing_leaves(device):
@@ -177,7 +183,7 @@ def test_softmin_wide_missing_leaves(device):
     f = eng.forward(_dev(leaves, device), _dev(cost, device, torch.float32), tau)
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     dc, _, _ = eng.backward(_dev(leaves, device), _dev(cost, device, torch.float32), tau, f.dp)
-    assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=offset_rtol(ref["dp"], tau))
+    assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=cond_rtol(ref["dp"], tau))
 
 
 @pytest.mark.parametrize("tau", [0.0, 0.5])

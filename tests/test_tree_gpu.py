@@ -189,11 +189,13 @@ def test_c5_scale_gram_properties(device):
     assert float(dA1[i, j]) == L - agree
 
 
-@pytest.mark.parametrize("gemm", ["x3", "f32"])
-def test_tree_optimizer_matches_oracle_loop(device, gemm):
+@pytest.mark.parametrize("gemm,L", [("x3", 52), ("f32", 52), ("x3", 51)])
+def test_tree_optimizer_matches_oracle_loop(device, gemm, L):
     """The fused device loop == oracle compute_loss + adam, step by step
-    (both GEMM precisions: f16x3 split products and f32 MFMA)."""
-    params, noise, seqs = _tree_case(16, 52, 4, 17)  # K = 208, a multiple of 16
+    (both GEMM precisions: f16x3 split products and f32 MFMA).  K = 208 is a
+    multiple of 16; K = 204 leaves a ragged last 16-column chunk, which the
+    x3 Gram masks (no silent fall back to f32)."""
+    params, noise, seqs = _tree_case(16, L, 4, 17)
     opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
                           lr=0.01, gemm=gemm)
     assert opt.gemm == gemm
@@ -211,7 +213,18 @@ def test_tree_optimizer_matches_oracle_loop(device, gemm):
         np.testing.assert_allclose(_n(opt.params[k]), p_ref[k], rtol=5e-5, atol=5e-6)
 
 
-@pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 8192, 128)])
+def test_tree_optimizer_x3_needs_aligned_rows_and_says_so(device):
+    """K = L*Q % 4 != 0 cannot feed the x3 GEMMs' 16-B row loads: the
+    optimiser warns and runs the f32 GEMMs (never silently)."""
+    params, noise, seqs = _tree_case(16, 33, 5, 3)  # K = 165
+    with pytest.warns(RuntimeWarning, match="multiple of 4"):
+        opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                              lr=0.01, gemm="x3")
+    assert opt.gemm == "f32"
+
+
+@pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 8192, 128),
+                                      (511, 25000, 256)])
 def test_gram_x3_stays_inside_its_workspace(device, N, K, skip):
     """The split-K Gram writes its partials only inside
     trex_tree_workspace_bytes(N, K) (a guard page of canary bytes after the
@@ -303,12 +316,14 @@ def test_gram_skip_keeps_cached_block(device):
 
 
 @pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 160, 130),
-                                      (100, 1024, 0), (64, 16, 0)])
+                                      (100, 1024, 0), (64, 16, 0), (511, 25000, 256),
+                                      (300, 1028, 130), (64, 20, 0)])
 def test_split_gram_and_mf_vs_fp64(device, N, K, skip):
     """f16x3 split-product Gram / MF (trex_tree_gram_skip_x3 /
     trex_tree_mf_rows_x3) vs fp64 at the f32 path's bar: softmax-like S
     (values spanning 1e-6 .. 1, one-hot rows) and M = diag(r+c) - (A+A^T)
-    with softmax rows of A."""
+    with softmax rows of A.  K = 25 000 is one rank's C5 site shard at N = 8
+    (6 250 sites x 4): K % 16 = 8, a ragged last chunk, like 1 028 and 20."""
     from trex_amd._lib import check, lib, ptr, stream_handle
 
     rng = np.random.default_rng(N + K)

@@ -85,6 +85,7 @@ SIGNATURES = {
                                       _c_f, _c_i, _p, _p, _p, _p, _p, _c_i64, _p]),
     "trex_tree_mf_rows": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _p, _p]),
     "trex_tree_gram_skip_x3": (_c_i, [_p, _c_i, _c_i64, _c_i, _c_f, _p, _p, _c_i64, _p]),
+    "trex_tree_gram_mirror": (_c_i, [_p, _c_i, _c_i, _p]),
     "trex_tree_mf_rows_x3": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p, _p]),
     "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),
     "trex_tree_constraint": (_c_i, [_p, _c_i, _c_f, _c_f, _p, _c_i, _p, _p, _p]),

@@ -509,15 +509,13 @@ constexpr int kPrefetchRows = 64;  // leaf tiles of <= 64 leaves are prefetched
 // adjacent tiles (shared L2 lines).  Each item is one (tree, 64*SPT-site
 // tile); the next item's leaf tile is loaded into registers while the
 // current one computes.
-// RES (fused PHASE 3 only): the LDS-resident variant.  Every internal D
-// vector of the item's tree stays in LDS ([n_int][64][Q], written once by the
-// forward, read by the adjoint), so the adjoint reads nothing from HBM; the
-// Sethi-Ullman slots then hold only cotangents.  Costs n_int*Q*256 B of LDS
-// per wave (31 KiB at 32 taxa: one wave per SIMD).
-template <int Q, int SPT, int MODE, int PHASE, bool LFAST, bool RES, bool RAGGED>
+// (An LDS-resident fused variant -- every internal D vector of the tree kept
+// in LDS, no adjoint re-read, one wave per SIMD -- measured 2.3x slower on the
+// C4 shard and on par for C2; removed in round 3 with the other A/B-only
+// variants)
+template <int Q, int SPT, int MODE, int PHASE, bool LFAST, bool RAGGED>
 __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
-  static_assert(!RAGGED || (SPT == 1 && !RES), "ragged batches use the SPT=1 re-reading kernels");
-  static_assert(!RES || (PHASE == 3 && SPT == 1), "resident mode is the fused SPT=1 kernel");
+  static_assert(!RAGGED || SPT == 1, "ragged batches use the SPT=1 kernels");
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
@@ -538,8 +536,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   float* tab = lds;
   float* slots = lds + kTabFloats;
   const int kRootSlot = A.n_slots;
-  float* dres = slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT;  // RES: [n_int][64][Q]
-  int8_t* lleaf = reinterpret_cast<int8_t*>(RES ? dres + (size_t)A.n_int * Q * kWave : dres);
+  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT);
 
   // ---- once per wave: leaf message table T[s][i] = C[i][s], T[Q][i] =
   // message of an all-1e5 row ----
@@ -667,10 +664,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
               for (int s = 0; s < SPT; ++s) d[c][j][s] = prev[j][s];
           } else if (kind == kKindInt) {
-            if constexpr (RES)
-              lds_get<Q, SPT>(dres, desc & 0xFFFF, lane, d[c]);
-            else
-              lds_get<Q, SPT>(slots, (desc >> 16) & 0xFF, lane, d[c]);
+            lds_get<Q, SPT>(slots, (desc >> 16) & 0xFF, lane, d[c]);
           } else {
             int code[SPT];
             if (kind == kKindLeaf) {
@@ -715,9 +709,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         const int row = stp.x & 0xFFFF;
         const int oslot = (stp.x >> 16) & 0xFF;
         bst_row<Q, SPT>(rdp, voff, row * rowbytes, dv);
-        if constexpr (RES) {
-          if (!(stp.w & kStepRoot)) lds_put<Q, SPT>(dres, row, lane, dv);
-        } else if (!(stp.w & kStepToNext) && oslot != 0xFF) {
+        if (!(stp.w & kStepToNext) && oslot != 0xFF) {
           lds_put<Q, SPT>(slots, oslot, lane, dv);
         }
 #pragma unroll
@@ -874,22 +866,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           }
         }
       };
-      if constexpr (RES) {
-        // D of the internal children from the resident table; the next
-        // step's program words are loaded one step ahead
-        I4 sn = load_step(prog, n_int - 1);
-        for (int k = n_int - 1; k >= 0; --k) {
-          const I4 cur = sn;
-          if (k >= 1) sn = load_step(prog, k - 1);
-          float cd[2][Q][SPT];
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int desc = c == 0 ? cur.y : cur.z;
-            if (((desc >> 24) & 3) == kKindInt) lds_get<Q, SPT>(dres, desc & 0xFFFF, lane, cd[c]);
-          }
-          bstep(cur, cd);
-        }
-      } else {
+      {
       float bufA[2][Q][SPT], bufB[2][Q][SPT];
       I4 sA = load_step(prog, n_int - 1);
       I4 sB = n_int > 1 ? load_step(prog, n_int - 2) : sA;
@@ -938,7 +915,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   } while (PERSIST && item < item_end);
 }
 
-template <int Q, int SPT, int MODE, int PHASE, bool RES = false, bool RAGGED = false>
+template <int Q, int SPT, int MODE, int PHASE, bool RAGGED = false>
 __device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds) {
   // leaf messages have the closed form C[i][code] when the 1e5 sentinel
   // dominates (hard: range(C) < 1e5; soft: exp(-(1e5 - range)/tau) < 2^-64)
@@ -947,9 +924,9 @@ __device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds
   const float range = cmax - cmin;
   const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
   if (lfast)
-    sankoff_body<Q, SPT, MODE, PHASE, true, RES, RAGGED>(A, lds);
+    sankoff_body<Q, SPT, MODE, PHASE, true, RAGGED>(A, lds);
   else
-    sankoff_body<Q, SPT, MODE, PHASE, false, RES, RAGGED>(A, lds);
+    sankoff_body<Q, SPT, MODE, PHASE, false, RAGGED>(A, lds);
 }
 
 template <int Q, int SPT, bool SOFT, int PHASE, bool RAGGED = false>
@@ -957,32 +934,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 
 void sankoff_kernel(KArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if constexpr (!SOFT) {
-    sankoff_dispatch_leaf<Q, SPT, kHard, PHASE, false, RAGGED>(A, lds);
+    sankoff_dispatch_leaf<Q, SPT, kHard, PHASE, RAGGED>(A, lds);
   } else {
     float cmin, cmax;
     cost_range<Q>(A.cost, cmin, cmax);
     if (use_ktrick(cmin, cmax, A.a))
-      sankoff_dispatch_leaf<Q, SPT, kSoftK, PHASE, false, RAGGED>(A, lds);
+      sankoff_dispatch_leaf<Q, SPT, kSoftK, PHASE, RAGGED>(A, lds);
     else
-      sankoff_dispatch_leaf<Q, SPT, kSoftDirect, PHASE, false, RAGGED>(A, lds);
-  }
-}
-
-// LDS-resident fused kernel (see sankoff_body, RES): occupancy is set by LDS
-// (one wave per SIMD at 32 taxa), so the register budget is generous
-template <int Q, bool SOFT>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 8)))
-void sankoff_res_kernel(KArgs A) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  if constexpr (!SOFT) {
-    sankoff_dispatch_leaf<Q, 1, kHard, 3, true>(A, lds);
-  } else {
-    float cmin, cmax;
-    cost_range<Q>(A.cost, cmin, cmax);
-    if (use_ktrick(cmin, cmax, A.a))
-      sankoff_dispatch_leaf<Q, 1, kSoftK, 3, true>(A, lds);
-    else
-      sankoff_dispatch_leaf<Q, 1, kSoftDirect, 3, true>(A, lds);
+      sankoff_dispatch_leaf<Q, SPT, kSoftDirect, PHASE, RAGGED>(A, lds);
   }
 }
 
@@ -1142,13 +1101,6 @@ size_t lds_bytes(int n_slots, int nl, int Q, int spt) {
   return (b + 15) & ~(size_t)15;
 }
 
-// LDS-resident fused kernel: the slot stack (cotangents) plus every internal
-// D vector of the tree
-size_t lds_res_bytes(int n_slots, int nl, int ni, int Q) {
-  const size_t b = (size_t)kTabFloats * 4 + (size_t)(n_slots + 1 + ni) * Q * kWave * 4 +
-                   (size_t)nl * kWave;
-  return (b + 15) & ~(size_t)15;
-}
 constexpr size_t kLdsPerCu = 160 * 1024;
 
 int device_cus() {
@@ -1160,38 +1112,6 @@ int device_cus() {
     return n;
   }();
   return cus;
-}
-
-// A/B-only path: with the wide_small_q policy every grid this would pick
-// (<= one wave per CU) already runs on the state-parallel kernel, so it is
-// reached only under TREX_WIDE_SMALLQ=0 (the tests' lane-per-site pass).
-// Resident mode trades the adjoint's HBM re-read of the DP table for LDS
-// occupancy.  Measured on the C4 shard (32 taxa, 31 KiB per wave, one wave
-// per SIMD) it is 2.3x slower than the re-reading kernel (410 vs 176 us: a
-// lone wave exposes every LDS / scalar-load / transcendental latency), so it
-// is taken only when the grid has at most one wave per CU anyway (C2-like
-// single trees, where it is on par or slightly faster).
-// TREX_RESIDENT=0 / 1 forces it off / on (whenever it fits; tuning).
-bool use_resident(size_t lds_res, int nitems) {
-  static const int forced = [] {
-    const char* e = std::getenv("TREX_RESIDENT");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (lds_res > kLdsPerCu || forced == 0) return false;
-  if (forced == 1) return true;
-  return (long)nitems <= (long)device_cus();
-}
-
-// sites per lane: 1 (measured fastest for the fused soft kernel: SPT=2
-// doubles the adjoint's VGPRs and halves occupancy).  TREX_SPT=2 forces two
-// sites per lane when L is even and the stack fits 12 KiB (tuning).
-int pick_spt(int L, int n_slots, int nl, int Q) {
-  static const int forced = [] {
-    const char* e = std::getenv("TREX_SPT");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced == 2 && L % 2 == 0 && lds_bytes(n_slots, nl, Q, 2) <= 12288) return 2;
-  return 1;
 }
 
 int hip_check(const char* fn) {
@@ -1239,11 +1159,7 @@ int persistent_grid(K kernel, size_t lds, int nitems) {
       if (ncache < 64) cache[ncache++] = Entry{(const void*)kernel, lds, occ};
     }
   }
-  static const int persist = [] {
-    const char* e = std::getenv("TREX_PERSIST");
-    return e ? std::atoi(e) : 1;
-  }();
-  const long resident = persist ? (long)cus * occ / 8 * 8 : (1L << 30);
+  const long resident = (long)cus * occ / 8 * 8;
   const long want = ((long)nitems + 7) / 8 * 8;
   return (int)std::max(8L, std::min(resident, want));
 }
@@ -1262,27 +1178,12 @@ void launch_phase(int phase, size_t lds, hipStream_t st, const KArgs& A) {
     go(sankoff_kernel<Q, SPT, SOFT, 3>);
 }
 
+// one site per lane (SPT = 1): two sites per lane doubled the adjoint's
+// VGPRs and was slower at every grid measured
 template <int Q>
-void dispatch_q(int phase, int spt, bool soft, size_t lds, hipStream_t st, const KArgs& A) {
-  if (spt == 2) {
-    if (soft) launch_phase<Q, 2, true>(phase, lds, st, A);
-    else launch_phase<Q, 2, false>(phase, lds, st, A);
-  } else {
-    if (soft) launch_phase<Q, 1, true>(phase, lds, st, A);
-    else launch_phase<Q, 1, false>(phase, lds, st, A);
-  }
-}
-
-template <int Q>
-void launch_res(bool soft, size_t lds, hipStream_t st, const KArgs& A) {
-  auto go = [&](auto kernel) {
-    if (lds > 65536)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kernel, dim3((A.nblocks + 7) / 8 * 8), dim3(kWave), lds, st, A);
-  };
-  if (soft) go(sankoff_res_kernel<Q, true>);
-  else go(sankoff_res_kernel<Q, false>);
+void dispatch_q(int phase, bool soft, size_t lds, hipStream_t st, const KArgs& A) {
+  if (soft) launch_phase<Q, 1, true>(phase, lds, st, A);
+  else launch_phase<Q, 1, false>(phase, lds, st, A);
 }
 
 // common entry: validates, fills KArgs, launches one phase
@@ -1379,12 +1280,9 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   }
   if ((int64_t)s.ni * L * Q * 4 > 0x7FFFFFF0LL)
     return set_error(TREX_E_UNSUPPORTED, "%s: one tree's DP table exceeds 2 GiB", fn);
-  const size_t lds_res = lds_res_bytes(n_slots, s.nl, s.ni, Q);
-  const bool res = phase == 3 && use_resident(lds_res, B * tiles_for(L, 1));
-  const int spt = res ? 1 : pick_spt(L, n_slots, s.nl, Q);
-  const int tiles = tiles_for(L, spt);
-  const size_t lds = res ? lds_res : lds_bytes(n_slots, s.nl, Q, spt);
-  if (lds > (res ? kLdsPerCu : 65536)) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
+  const int tiles = tiles_for(L, 1);
+  const size_t lds = lds_bytes(n_slots, s.nl, Q, 1);
+  if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
   if ((int64_t)B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
   KArgs A;
   A.rmeta = nullptr;
@@ -1414,18 +1312,10 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   A.part_dc = A.part_tree + A.nblocks;
   const bool soft = tau > 0.0f;
   hipStream_t st = (hipStream_t)stream;
-  if (res) {
-    switch (Q) {
-      case 2: launch_res<2>(soft, lds, st, A); break;
-      case 3: launch_res<3>(soft, lds, st, A); break;
-      case 4: launch_res<4>(soft, lds, st, A); break;
-    }
-  } else {
-    switch (Q) {
-      case 2: dispatch_q<2>(phase, spt, soft, lds, st, A); break;
-      case 3: dispatch_q<3>(phase, spt, soft, lds, st, A); break;
-      case 4: dispatch_q<4>(phase, spt, soft, lds, st, A); break;
-    }
+  switch (Q) {
+    case 2: dispatch_q<2>(phase, soft, lds, st, A); break;
+    case 3: dispatch_q<3>(phase, soft, lds, st, A); break;
+    case 4: dispatch_q<4>(phase, soft, lds, st, A); break;
   }
   if (int e = hip_check(fn)) return e;
   return partial_reduce(fn, A.part_tree, A.part_dc, B, tiles, Q, phase, tree_score, d_cost, stream);
@@ -1522,29 +1412,10 @@ extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, con
   if (!plan || !cost || !dp || !anc_states)
     return set_error(TREX_E_ARG, "trex_sankoff_backtrack: null pointer argument");
   const int32_t* bt32 = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 4;
-  // split-lane kernel (wide_backtrack4_kernel, 4 lanes per site for Q <= 4);
-  // TREX_BT4=0 keeps the sites-per-lane kernel below (A/B, tested)
-  const char* e4 = std::getenv("TREX_BT4");
-  if (Q > 4 || !(e4 && e4[0] == '0'))
-    return wide_backtrack(bt32, cost, dp, B, L, s.ni, Q, anc_states, stream);
-  const int spt = (L % 4 == 0) ? 4 : 1;
-  const int tiles = tiles_for(L, spt);
-  hipStream_t st = (hipStream_t)stream;
-  const int2* bt = reinterpret_cast<const int2*>(bt32);
-#define TREX_BT(QQ)                                                                            \
-  if (spt == 4)                                                                                \
-    hipLaunchKernelGGL((sankoff_backtrack_kernel<QQ, 4>), dim3(B * tiles), dim3(kWave), 0, st, \
-                       bt, cost, dp, s.ni, L, tiles, anc_states);                              \
-  else                                                                                         \
-    hipLaunchKernelGGL((sankoff_backtrack_kernel<QQ, 1>), dim3(B * tiles), dim3(kWave), 0, st, \
-                       bt, cost, dp, s.ni, L, tiles, anc_states);
-  switch (Q) {
-    case 2: TREX_BT(2) break;
-    case 3: TREX_BT(3) break;
-    case 4: TREX_BT(4) break;
-  }
-#undef TREX_BT
-  return hip_check("trex_sankoff_backtrack");
+  // every uniform batch: the split-lane kernels of sankoff_wide.hip (4 lanes
+  // per site for Q <= 4, 8 for Q <= 32, one lane per site for codons); the
+  // sites-per-lane sankoff_backtrack_kernel serves ragged Q <= 4 batches
+  return wide_backtrack(bt32, cost, dp, B, L, s.ni, Q, anc_states, stream);
 }
 
 extern "C" int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,

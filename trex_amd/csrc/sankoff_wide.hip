@@ -813,9 +813,11 @@ int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t st
 
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream) {
-  const char* e4 = std::getenv("TREX_BT4");  // A/B: 0 = one lane per site, 4 = four lanes
-  // 8 lanes per site for Q > 4; Q <= 4 (one state per lane): 4
-  const int lps = ((e4 && e4[0] == '4') || Q <= 4) ? 4 : 8;
+  // TREX_BT4=0 forces the one-lane-per-site kernel (live for codons, ragged
+  // batches and trees too deep for the split kernel's LDS; the tests run it
+  // on Q <= 32 too).  8 lanes per site for Q > 4; Q <= 4 (one state per lane): 4
+  const char* e4 = std::getenv("TREX_BT4");
+  const int lps = Q <= 4 ? 4 : 8;
   if (Q <= 32 && !(e4 && e4[0] == '0') && (int64_t)ni * L * Q * 4 <= 0x7FFFFFF0LL &&
       32 * 32 * 4 + (size_t)ni * (kWave / lps) <= 65536) {
     const int spw = kWave / lps;

@@ -513,10 +513,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       pf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((rb + kRowsPerPass * i) * K + 4 * sub) * 4,
                                                     c * 64, 0);
   };
-  auto stage = [&](unsigned char* buf) {
+  // K % 16 != 0 (K % 4 == 0): the last chunk's columns past K hold the next
+  // row's first values (or read out of bounds: 0); staged as zeros, they add
+  // nothing to any product
+  auto stage = [&](unsigned char* buf, int c) {
+    const bool kv = 16 * c + 4 * sub < K;
 #pragma unroll
     for (int i = 0; i < kG3Rows / kRowsPerPass; ++i)
-      g3_stage(buf, rb + kRowsPerPass * i, sub, pf[i], sc);
+      g3_stage(buf, rb + kRowsPerPass * i, sub, kv ? pf[i] : (u32x4){0u, 0u, 0u, 0u}, sc);
   };
   const int lofs = r * kG3Stride + 16 * h;
   auto compute = [&](const unsigned char* buf) {
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   if (c_lo < c_hi) {
     gload(c_lo);
-    stage(lds3);
+    stage(lds3, c_lo);
     if (c_lo + 1 < c_hi) gload(c_lo + 1);
   }
   lds_barrier();
@@ -548,7 +552,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     unsigned char* nb = lds3 + (((c - c_lo) & 1) ^ 1) * kG3Buf;
     compute(cb);
     if (c + 1 < c_hi) {
-      stage(nb);
+      stage(nb, c + 1);
       if (c + 2 < c_hi) gload(c + 2);
     }
     lds_barrier();
@@ -642,6 +646,17 @@ __global__ __launch_bounds__(256) void surrogate_combine_kernel(const float* __r
   }
 }
 
+// G[i][j] = G[j][i] for i < row0 <= j: after a site-sharded all-reduce of
+// the rows [row0, N) only, the leaf rows' ancestor columns take the reduced
+// values (the leaf x leaf block [0, row0)^2 is a cached global constant)
+__global__ __launch_bounds__(256) void gram_mirror_kernel(float* __restrict__ G, int N, int row0) {
+  const int64_t n = (int64_t)row0 * (N - row0);
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int i = (int)(t / (N - row0)), j = row0 + (int)(t % (N - row0));
+    G[(size_t)i * N + j] = G[(size_t)j * N + i];
+  }
+}
+
 __global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict__ v, int n,
                                                       float scale, float* __restrict__ out,
                                                       int accumulate) {
@@ -658,7 +673,8 @@ __global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict_
 // once.
 // ---------------------------------------------------------------------------
 
-// v2 dF = M F (the f32-MFMA path; the f16x3 one with TREX_GRAM_V2=1): 16 n
+// v2 dF = M F (the f32-MFMA path; X3 = the first f16x3 version, kept
+// instantiable for A/B builds, unused since MF v3): 16 n
 // per step, next step's operands requested before this
 // step's 32 MFMAs (ping-pong registers, unrolled by two).  Lane (r, h)
 // supplies M[row][nb + 8h + t] and F[nb + 8h + t][col]; rows / n / cols past
@@ -1428,7 +1444,8 @@ GramPlan gram_plan(int N, int64_t K, bool symmetric = false, int t0 = 0) {
   return g;
 }
 
-// v3 plan (symmetric, N <= 512, K % 16 == 0): 32-row strips, tiles per
+// v3 plan (symmetric, N <= 512, K % 4 == 0: 16-B aligned rows; a ragged
+// last 16-column chunk is zero-masked in the kernel): 32-row strips, tiles per
 // group of 8 waves x 13, about one workgroup per CU
 struct Gram3Plan {
   int ns, t0s, ntiles, ngroups, ksplit, nchunks;
@@ -1440,11 +1457,11 @@ Gram3Plan gram3_plan(int N, int64_t K, int t0s) {
   g.ntiles = 0;
   for (int a = 0; a < g.ns; ++a) g.ntiles += sym_row_len(a, g.ns, t0s);
   g.ngroups = std::max(1, (g.ntiles + kG3Waves * kG3Tiles - 1) / (kG3Waves * kG3Tiles));
-  g.nchunks = (int)(K / 16);
+  g.nchunks = (int)((K + 15) / 16);
   g.ksplit = std::max(1, std::min(g.nchunks, std::max(1, 256 / g.ngroups)));
   return g;
 }
-bool gram3_ok(int N, int64_t K) { return N <= kG3Rows && K % 16 == 0 && (int64_t)N * K * 4 < 0x7FFFFFF0LL; }
+bool gram3_ok(int N, int64_t K) { return N <= kG3Rows && K % 4 == 0 && (int64_t)N * K * 4 < 0x7FFFFFF0LL; }
 }  // namespace
 
 namespace {
@@ -1483,16 +1500,6 @@ float split_scale(float max_abs) {
   return std::ldexp(1.0f, 14 - (int)std::ceil(std::log2((double)max_abs)));
 }
 
-// TREX_GRAM_V2=1 keeps the v2 x3 Gram and MF kernels (one wave per 64x64
-// tile, operands straight from L2), for A/B
-bool gram_v2_forced() {
-  static const bool f = [] {
-    const char* e = std::getenv("TREX_GRAM_V2");
-    return e && e[0] == '1';
-  }();
-  return f;
-}
-
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
          hipStream_t st, int t0 = 0, float x3_max = 0.0f) {
@@ -1500,7 +1507,7 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
   if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
-  if (symmetric && X == Y && x3_max > 0.0f && gram3_ok(N, K) && !gram_v2_forced()) {
+  if (symmetric && X == Y && x3_max > 0.0f && gram3_ok(N, K)) {
     const Gram3Plan p = gram3_plan(N, K, 2 * t0);
     if (p.ntiles == 0) return TREX_OK;
     static bool lds_set = false;
@@ -1741,12 +1748,22 @@ extern "C" int trex_tree_gram_skip_x3(const float* S, int N, int64_t K, int skip
   if (!S || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF || skip_rows < 0 ||
       skip_rows > N || !pos_finite_f32(max_abs))
     return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3: bad arguments");
-  if (K % 16 != 0)
-    return set_error(TREX_E_UNSUPPORTED, "trex_tree_gram_skip_x3: K = L*Q must be a multiple of 16");
+  if (K % 4 != 0)
+    return set_error(TREX_E_UNSUPPORTED, "trex_tree_gram_skip_x3: K = L*Q must be a multiple of 4");
   if (workspace_bytes < trex_tree_workspace_bytes(N, K))
     return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3: workspace too small");
   return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream,
               skip_rows / 64, max_abs);
+}
+
+extern "C" int trex_tree_gram_mirror(float* G, int N, int row0, void* stream) {
+  if (!G || N <= 0 || row0 < 0 || row0 > N)
+    return set_error(TREX_E_ARG, "trex_tree_gram_mirror: bad arguments");
+  if (row0 == 0 || row0 == N) return TREX_OK;
+  const int64_t n = (int64_t)row0 * (N - row0);
+  hipLaunchKernelGGL(gram_mirror_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)),
+                     dim3(256), 0, (hipStream_t)stream, G, N, row0);
+  return tree_hip_check("trex_tree_gram_mirror");
 }
 
 extern "C" int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
@@ -1789,38 +1806,34 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
     return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3: bad arguments");
   if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
     return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows_x3: S exceeds 2 GiB");
-  if (!gram_v2_forced()) {
-    // column tiles per workgroup: fewest rounds x tiles over one workgroup per CU
-    const int64_t ct = (K + 31) / 32;
-    const int rg = (nrows + 255) / 256;
-    int best = 5;
-    int64_t best_cost = INT64_MAX;
-    for (int tpc : {5, 4}) {
-      const int64_t wgs = (ct + tpc - 1) / tpc * rg;
-      const int64_t cost = (wgs + cu_count() - 1) / cu_count() * tpc;
-      if (cost < best_cost) { best_cost = cost; best = tpc; }
-    }
-    auto go = [&](auto kernel, int tpc, int lds) {
-      if (lds > 65536)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      const int nch = (int)((ct + tpc - 1) / tpc);
-      // one persistent workgroup per CU (per row group)
-      const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
-      hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(512), lds, (hipStream_t)stream, M, S, N,
-                         (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
-                         split_scale(max_abs_s));
-    };
-    if (best == 5) go(mf_kernel3<5>, 5, 2 * (2 * 32 * 320 + 256 * kMfStride));
-    else go(mf_kernel3<4>, 4, 2 * (2 * 32 * 320 + 256 * kMfStride));
-    return tree_hip_check("trex_tree_mf_rows_x3");
+  // float4 operand loads: rows must start 16-B aligned (the last column tile
+  // may be ragged: its columns past K are computed from the next row's data
+  // and never stored)
+  if (K % 4 != 0)
+    return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows_x3: K = L*Q must be a multiple of 4");
+  // column tiles per workgroup: fewest rounds x tiles over one workgroup per CU
+  const int64_t ct = (K + 31) / 32;
+  const int rg = (nrows + 255) / 256;
+  int best = 5;
+  int64_t best_cost = INT64_MAX;
+  for (int tpc : {5, 4}) {
+    const int64_t wgs = (ct + tpc - 1) / tpc * rg;
+    const int64_t cost = (wgs + cu_count() - 1) / cu_count() * tpc;
+    if (cost < best_cost) { best_cost = cost; best = tpc; }
   }
-  const int nrowt = (nrows + 63) / 64;
-  const int ncolb = (int)((K + 63) / 64);
-  const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
-  hipLaunchKernelGGL(mf_kernel2<true>, dim3(blocks), dim3(kWave), 0, (hipStream_t)stream, M, S, N,
-                     (int)K, row0, nrows, nrowt, ncolb, dS_rows, split_scale(max_abs_m),
-                     split_scale(max_abs_s));
+  auto go = [&](auto kernel, int tpc, int lds) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    const int nch = (int)((ct + tpc - 1) / tpc);
+    // one persistent workgroup per CU (per row group)
+    const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
+    hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(512), lds, (hipStream_t)stream, M, S, N,
+                       (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
+                       split_scale(max_abs_s));
+  };
+  if (best == 5) go(mf_kernel3<5>, 5, 2 * (2 * 32 * 320 + 256 * kMfStride));
+  else go(mf_kernel3<4>, 4, 2 * (2 * 32 * 320 + 256 * kMfStride));
   return tree_hip_check("trex_tree_mf_rows_x3");
 }
 

@@ -50,8 +50,10 @@ class GramReducer:
 
     compute_surrogate_cost (src/trex/tree.py:199-209) depends on the sites only
     through G = S S^T (with E = diag G), a sum over sites; each rank computes
-    G over its block of sites and one all-reduce (N*N fp32, 1.04 MB at
-    N = 511) makes every rank's G the full one.  The combine (value, dA,
+    G over its block of sites and one all-reduce makes every rank's G the
+    full one: the whole N x N matrix once (1.04 MB at N = 511), then per step
+    only the rows the step recomputes (``G[row0:]``, the ancestor rows x all
+    columns: 0.52 MB; TreeOptimizer mirrors them into the leaf rows).  The combine (value, dA,
     M = diag(r+c) - (A+A^T)), the tree_params gradient and their Adam update
     are then identical on all ranks; dS = M S_local stays local.
     """
@@ -62,6 +64,8 @@ class GramReducer:
     def __call__(self, G):
         import torch.distributed as dist
 
+        if not G.is_contiguous():
+            raise ValueError("GramReducer: G (or its row block) must be contiguous")
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(G, group=self.group)
         return G

@@ -301,7 +301,9 @@ class TreeOptimizer:
 
     Site sharding (``group``): each rank holds a contiguous block of sites
     (its leaf one-hot rows and ancestor logits for those sites).  The only
-    exchange is an all-reduce of the N x N Gram matrix; every rank then
+    exchange is an all-reduce of the Gram rows that change (the ancestor
+    rows x all columns; the leaf x leaf block is reduced once at
+    construction and cached); every rank then
     computes the same loss, dA and tree_params update, and updates its own
     ancestor logits.  With ``clip_norm`` (the evals path's
     clip_by_global_norm(1.0), src/trex/evals/benchmark.py:70-71) one more
@@ -350,16 +352,28 @@ class TreeOptimizer:
         self._s_temperature = None  # temperature the S ancestor rows were computed with
         if gemm not in ("x3", "f32"):
             raise ValueError("gemm must be 'x3' or 'f32'")
-        # the split Gram needs K = L*Q % 16 == 0; otherwise fall back to f32
-        self.gemm = gemm if (gemm == "f32" or self.K % 16 == 0) else "f32"
+        # the split-product GEMMs load 16-B row pieces: K = L*Q % 4 == 0 (a
+        # ragged last K chunk is masked in the kernels, so a site shard of
+        # any length works when Q % 4 == 0)
+        self.gemm = gemm
+        if gemm == "x3" and self.K % 4 != 0:
+            import warnings
+
+            warnings.warn(f"TreeOptimizer: K = L*Q = {self.K} is not a multiple of 4; the f16x3 "
+                          "GEMMs need 16-B aligned rows, running the f32 MFMA GEMMs instead",
+                          RuntimeWarning, stacklevel=2)
+            self.gemm = "f32"
         # the leaf x leaf block of G = S S^T is constant (leaf rows are data):
-        # computed once here, skipped by every step's Gram.  With site
-        # sharding the Gram is all-reduced in place, so it is recomputed.
-        self.skip_rows = 0
-        if group is None:
-            check(lib().trex_tree_gram(ptr(self.S), self.N, self.K, ptr(self.G), ptr(self.ws),
-                                       self.ws.numel(), stream_handle(dev)))
-            self.skip_rows = self.n_leaf
+        # computed once here (all-reduced once under site sharding), skipped
+        # by every step's Gram.  Rows [g_row0, N) are recomputed each step;
+        # under sharding only they are all-reduced, then mirrored into the
+        # leaf rows' ancestor columns (trex_tree_gram_mirror).
+        check(lib().trex_tree_gram(ptr(self.S), self.N, self.K, ptr(self.G), ptr(self.ws),
+                                   self.ws.numel(), stream_handle(dev)))
+        if self.reducer is not None:
+            self.reducer(self.G)
+        self.skip_rows = self.n_leaf
+        self.g_row0 = (self.skip_rows // 64) * 64
 
     def step(self, temperature: float, noise, next_temperature=None):
         """One optimisation step; returns the (device) loss before the update.
@@ -388,7 +402,8 @@ class TreeOptimizer:
             check(L_.trex_tree_gram_skip(ptr(self.S), N, K, self.skip_rows, ptr(self.G),
                                          ptr(self.ws), self.ws.numel(), st))
         if self.reducer is not None:
-            self.reducer(self.G)
+            self.reducer(self.G[self.g_row0:])
+            check(L_.trex_tree_gram_mirror(ptr(self.G), N, self.g_row0, st))
         check(L_.trex_tree_surrogate_combine(ptr(self.A), ptr(self.G), N, ptr(self.loss),
                                              ptr(self.dA), ptr(self.M), ptr(self.ws), st))
         check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
