@@ -12,16 +12,19 @@
  * hard min (:68) with JAX's tie-averaged min gradient; tau > 0 the softmin
  * relaxation of DESIGN.md, in the per-row stabilised form (no factoring).
  *
- * Two instantiations of one body (cpu_port_impl.h):
- *   sankoff_cpu_fwd_bwd    fp32 arithmetic, as trex computes -- the timed
- *                          CPU baseline ("port");
- *   sankoff_cpu64_fwd_bwd  fp64 arithmetic -- the checker for GPU results at
- *                          sizes the numpy oracle cannot hold (C4's 1024-tree
- *                          batch), pinned to oracle/softmin_ref.py by
- *                          tests/test_cpu_port_cpu.py.
- * Built without -ffast-math (the INFINITY sentinels need IEEE semantics);
- * only reassociation is allowed, so the site loops vectorise.
+ * Two instantiations of one body (cpu_port_impl.h), in two translation
+ * units with their own flags (oracle/Makefile):
+ *   sankoff_cpu_fwd_bwd    (this file) fp32 arithmetic, as trex computes --
+ *                          the timed CPU baseline ("port"), built with
+ *                          -ffast-math so its exp / log vectorise (glibc's
+ *                          vector math needs it); every sentinel is finite
+ *                          (1e5, FLT_MAX), so finite-math is sound here;
+ *   sankoff_cpu64_fwd_bwd  (cpu_port64.c) fp64 arithmetic, strict IEEE --
+ *                          the checker for GPU results at sizes the numpy
+ *                          oracle cannot hold (C4's 1024-tree batch).
+ * Both are pinned to oracle/softmin_ref.py by tests/test_cpu_port_cpu.py.
  */
+#include <float.h>
 #include <math.h>
 #include <omp.h>
 #include <stdint.h>
@@ -32,20 +35,9 @@
 #define SENT 1e5
 
 #define REAL float
+#define REAL_BIG FLT_MAX
 #define EXP expf
 #define LOG logf
 #define FN sankoff_cpu_fwd_bwd
 #define NM(x) x##_f32
-#include "cpu_port_impl.h"
-#undef REAL
-#undef EXP
-#undef LOG
-#undef FN
-#undef NM
-
-#define REAL double
-#define EXP exp
-#define LOG log
-#define FN sankoff_cpu64_fwd_bwd
-#define NM(x) x##_f64
 #include "cpu_port_impl.h"

@@ -4,8 +4,10 @@
  * REAL = double (the fp64 checker the full-batch GPU tests compare against).
  * TEST INFRASTRUCTURE / CPU BASELINE ONLY -- see cpu_port.c.
  *
- * Before including: REAL, EXP, LOG, FN (exported name), NM(x) (suffix for
- * the file-local helpers).
+ * Before including: REAL, REAL_BIG (a finite "+infinity" for min scans --
+ * the fp32 baseline is built with -ffast-math, under which IEEE infinities
+ * are undefined), EXP, LOG, FN (exported name), NM(x) (suffix for the
+ * file-local helpers).
  */
 
 static inline int NM(classify)(int c, int node, int nl) {
@@ -38,7 +40,7 @@ static void NM(message)(int Q, int nb, const REAL* cost, REAL tau, const REAL* d
   for (int i = 0; i < Q; ++i) {
     REAL x[32][BLK];
     REAL mn[BLK];
-    for (int s = 0; s < nb; ++s) mn[s] = (REAL)INFINITY;
+    for (int s = 0; s < nb; ++s) mn[s] = REAL_BIG;
     for (int j = 0; j < Q; ++j)
       for (int s = 0; s < nb; ++s) {
         x[j][s] = cost[i * Q + j] + d[j * BLK + s];
@@ -131,7 +133,7 @@ int FN(const int32_t* children, const int8_t* leaves, const float* cost_in, int 
       memset(G, 0, sizeof(REAL) * ni * Q * BLK);
       REAL* Gr = G + (size_t)(ni - 1) * Q * BLK;
       for (int s = 0; s < nb; ++s) {
-        REAL mn = (REAL)INFINITY;
+        REAL mn = REAL_BIG;
         for (int i = 0; i < Q; ++i) mn = Dr[i * BLK + s] < mn ? Dr[i * BLK + s] : mn;
         if (tau > 0) {
           REAL sum = 0;
