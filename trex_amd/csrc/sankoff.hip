@@ -1274,8 +1274,18 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
     c.d_cost = d_cost;
     c.workspace = workspace;
     c.stream = stream;
-    if (use_staged(B, L, Q, s.ni, s.nl, phase))
-      return staged_run(fn, c, plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 6);
+    const int32_t* staged = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 6;
+    if (mx_eligible(c)) {
+      // the matrix-core kernel first (sankoff_mx.hip); its device flag (a
+      // word in the workspace's tail slack) tells the state-parallel launch
+      // below whether to run
+      int* flag = reinterpret_cast<int*>(static_cast<char*>(workspace) +
+                                         wide_workspace_bytes(B, L, Q) - 128);
+      if (int e = mx_run(fn, c, staged, flag)) return e;
+      c.mx_flag = flag;
+      c.mx_tiles = mx_tiles(L);
+    }
+    if (use_staged(B, L, Q, s.ni, s.nl, phase)) return staged_run(fn, c, staged);
     return wide_run(fn, c);
   }
   if ((int64_t)s.ni * L * Q * 4 > 0x7FFFFFF0LL)

@@ -56,6 +56,7 @@ struct SArgs {
   int tail;           // 1: the last workgroup reduces the partials
   float* tree_score;  // [B]
   float* d_cost;      // [Q][Q]
+  const int* skip = nullptr;  // matrix-core kernel's flag: set -> it handled this launch
 };
 
 #ifdef TREX_STAGED_TIMING
@@ -527,6 +528,7 @@ constexpr int staged_min_waves() { return G == 4 ? 6 : 1; }
 template <int G, bool SOFT, int PHASE>
 __global__ __launch_bounds__(kSW* kWave, staged_min_waves<G>()) void sankoff_staged_kernel(SArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (A.skip && __hip_atomic_load(A.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int Q = A.Q;
   const int i = (threadIdx.x % kWave) % G;
   float cmin, cmax;
@@ -635,7 +637,10 @@ int staged_run(const char* fn, const WideCall& c, const int32_t* staged) {
   // in-kernel tail for small reductions (C2: 17 entries x 625 items);
   // larger ones go to the separate fixed-order reduce kernel
   const int64_t nent = ((c.phase & 1) ? c.B : 0) + ((c.phase & 2) ? (int64_t)c.Q * c.Q : 0);
-  A.tail = nent * nb <= (int64_t)1 << 16;
+  // (behind the matrix-core kernel the separate reduce runs: it knows, from
+  // the device flag, whose partials to sum)
+  A.tail = !c.mx_flag && nent * nb <= (int64_t)1 << 16;
+  A.skip = c.mx_flag;
   hipStream_t st = (hipStream_t)c.stream;
   const int grid = (int)nb;
   switch (wide_group(c.Q)) {
@@ -649,7 +654,7 @@ int staged_run(const char* fn, const WideCall& c, const int32_t* staged) {
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
   if (A.tail) return TREX_OK;  // partials reduced by the kernel's last workgroup
   return partial_reduce(fn, A.part_tree, A.part_dc, c.B, tiles, c.Q, c.phase, c.tree_score,
-                        c.d_cost, c.stream);
+                        c.d_cost, c.stream, nullptr, 0, 0, 1, c.mx_flag, c.mx_tiles);
 }
 
 }  // namespace trex

@@ -51,6 +51,7 @@ struct WArgs {
   const int* rmeta;
   const int* ritem;
   int wpi;
+  const int* skip = nullptr;  // matrix-core kernel's flag: set -> it handled this launch
 };
 
 // LDS map (floats): 4 exchange buffers [4][64], leaf message table
@@ -351,6 +352,7 @@ constexpr int wide_min_blocks() { return (G == 20 && (PHASE & 2)) ? TREX_WIDE_MI
 template <int G, bool SOFT, int PHASE, bool RAGGED = false>
 __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_wide_kernel(WArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  if (A.skip && __hip_atomic_load(A.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int Q = A.Q;
   const int i = threadIdx.x % G;
   float cmin, cmax;
@@ -387,9 +389,16 @@ __global__ __launch_bounds__(kReduceThreads) void wide_reduce_kernel(const doubl
                                                           float* __restrict__ d_cost,
                                                           const int* __restrict__ first,
                                                           int first_stride, int items,
-                                                          int first_scale) {
+                                                          int first_scale, const int* mx_flag,
+                                                          int mx_tiles) {
   __shared__ double red[kReduceThreads];
   const int b = blockIdx.x;
+  if (mx_flag && __hip_atomic_load(mx_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    // the matrix-core kernel's partials (sankoff_mx.hip): mx_tiles per tree,
+    // its dC block right after its B * mx_tiles tree partials
+    tiles = mx_tiles;
+    part_dc = part_tree + (size_t)B * mx_tiles;
+  }
   const double* src;
   int n;
   float* dst;
@@ -705,6 +714,7 @@ int wide_run(const char* fn, const WideCall& c) {
   A.rmeta = nullptr;
   A.ritem = nullptr;
   A.wpi = 0;
+  A.skip = c.mx_flag;
   const int64_t nb = (int64_t)c.B * tiles;
   A.part_tree = static_cast<double*>(c.workspace);
   A.part_dc = A.part_tree + nb;
@@ -721,7 +731,7 @@ int wide_run(const char* fn, const WideCall& c) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
   return partial_reduce(fn, A.part_tree, A.part_dc, c.B, tiles, c.Q, c.phase, c.tree_score,
-                        c.d_cost, c.stream);
+                        c.d_cost, c.stream, nullptr, 0, 0, 1, c.mx_flag, c.mx_tiles);
 }
 
 // waves per 64-site ragged item: ceil(64 / sites per wave)
@@ -762,6 +772,7 @@ int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const i
   A.rmeta = rmeta;
   A.ritem = ritem;
   A.wpi = wpi;
+  A.skip = nullptr;  // ragged batches never run the matrix-core kernel
   const int grid = (int)(items * wpi);
   A.part_tree = static_cast<double*>(c.workspace);
   A.part_dc = A.part_tree + grid;
@@ -781,13 +792,14 @@ int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const i
 
 int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
                    int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream,
-                   const int* first, int first_stride, int items, int first_scale) {
+                   const int* first, int first_stride, int items, int first_scale,
+                   const int* mx_flag, int mx_tiles) {
   const bool do_tree = (phase & 1) != 0;
   const bool do_dc = (phase & 2) != 0;
   const int rgrid = (do_tree ? B : 0) + (do_dc ? Q * Q : 0);
   hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(kReduceThreads), 0, (hipStream_t)stream,
                      part_tree, part_dc, B, tiles, Q * Q, do_tree ? 1 : 0, tree_score, d_cost,
-                     first, first_stride, items, first_scale);
+                     first, first_stride, items, first_scale, mx_flag, mx_tiles);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
   return TREX_OK;

@@ -83,6 +83,11 @@ struct WideCall {
   float* d_cost;
   void* workspace;
   void* stream;
+  // set when the matrix-core kernel (sankoff_mx.hip) ran first: the device
+  // word it wrote (1: it handled the launch -- the state-parallel kernels
+  // exit at once, the reduce sums its mx_tiles partials per tree)
+  const int* mx_flag = nullptr;
+  int mx_tiles = 0;
 };
 constexpr int kWideMaxQ = 64;
 constexpr int kRaggedMeta = 12;  // ints per tree record of a ragged plan (plan.cpp)  // leaf codes and ancestral states are int8
@@ -100,15 +105,22 @@ int staged_run(const char* fn, const WideCall& c, const int32_t* staged);
 // (ragged batches: first[b * first_stride] is tree b's first item, items the
 // total; tiles is then unused)
 // (first_scale: partials per item, the wide kernel's waves per ragged item)
+// (mx_flag / mx_tiles: when *mx_flag is set on the device, the partials are
+// the matrix-core kernel's, mx_tiles per tree)
 int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
                    int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream,
                    const int* first = nullptr, int first_stride = 0, int items = 0,
-                   int first_scale = 1);
+                   int first_scale = 1, const int* mx_flag = nullptr, int mx_tiles = 0);
 // ragged batches with Q > 4 on the wide kernel (rmeta / ritem: the plan's
 // records and item table; c.nl = max leaves, c.L unused)
 int64_t wide_ragged_workspace_bytes(int64_t items, int Q);
 int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const int* ritem,
                     int64_t items);
+// matrix-core kernel for the factored softmin, 4 < Q <= 20 (sankoff_mx.hip)
+bool mx_eligible(const WideCall& c);
+int mx_tiles(int L);
+size_t mx_lds_bytes(int ni, int nl, int Q);
+int mx_run(const char* fn, const WideCall& c, const int32_t* staged, int* flag);
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream);
 int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,
