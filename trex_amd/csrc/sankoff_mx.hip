@@ -55,6 +55,7 @@ namespace {
 constexpr int kMW = kStageWaves;  // waves per workgroup
 constexpr int kMS = 16;           // sites per work item (the MFMA's N)
 constexpr int kMxMaxQ = 20;
+constexpr int kXRow = 33;  // outer-product scratch row (32 states + 1 pad: conflict-free reads)
 
 typedef float mf4 __attribute__((ext_vector_type(4)));
 
@@ -246,7 +247,9 @@ __device__ __forceinline__ void mx_body(const MArgs& A, float* lds) {
   float* sinv = ik + Q * Q;
   float* kval = sinv + kMxMaxQ;  // K [Q][Q]
   float* cst = kval + kMxMaxQ * kMxMaxQ;  // the cost matrix, moved out of the slot area
-  int8_t* lleaf = reinterpret_cast<int8_t*>(cst + kMxMaxQ * kMxMaxQ);
+  float* xscr = cst + kMxMaxQ * kMxMaxQ;  // per-wave outer-product scratch [kMW][2][16][kXRow]
+  int8_t* lleaf = reinterpret_cast<int8_t*>(xscr + kMW * 2 * kMS * kXRow);
+  for (int e = threadIdx.x; e < kMW * 2 * kMS * kXRow; e += kMW * kWave) xscr[e] = 0.0f;
   for (int e = threadIdx.x; e < Q * Q; e += kMW * kWave) cst[e] = cl[e];
   __syncthreads();
   auto slot = [&](int r, int t) -> float& { return slots[((size_t)r * P + t) * kWave + lane]; };
@@ -490,11 +493,42 @@ __device__ __forceinline__ void mx_body(const MArgs& A, float* lds) {
     if constexpr (FWD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     MX_STAMP(8);
-    float acc[P][kMxMaxQ];  // acc[t][j]: row g P + t, column j, factored (x K_ij at the end)
+    // dC accumulates on the matrix core: per child, the wave's (r, u) pairs
+    // go through its LDS scratch [16 sites][33] (r | u), read back as
+    // 16x16x4 f32 operands (k = 4 sites) -- acc_ij += sum_sites r_i u_j,
+    // 2 x 2 blocks of 16 x 16 (i, j < 32), x K_ij at the end (fp64)
+    mf4 oacc[2][2];
 #pragma unroll
-    for (int t = 0; t < P; ++t)
+    for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-      for (int j = 0; j < kMxMaxQ; ++j) acc[t][j] = 0.0f;
+      for (int jb = 0; jb < 2; ++jb) oacc[ib][jb] = mf4{0.0f, 0.0f, 0.0f, 0.0f};
+    float* xr = xscr + (size_t)wv * 2 * kMS * kXRow;
+    float* xu = xr + kMS * kXRow;
+    auto outer = [&](const float (&r)[P], const float (&u)[P]) {
+#pragma unroll
+      for (int t = 0; t < P; ++t)
+        if (valid[t]) {
+          xr[s16 * kXRow + qg * P + t] = r[t];
+          xu[s16 * kXRow + qg * P + t] = u[t];
+        }
+      wave_sync();
+#pragma unroll
+      for (int kc = 0; kc < kMS / 4; ++kc) {
+        const int pr = (4 * kc + (lane >> 4)) * kXRow + (lane & 15);
+        float ra[2], ub[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          ra[h] = xr[pr + 16 * h];
+          ub[h] = xu[pr + 16 * h];
+        }
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb)
+            oacc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[ib], ub[jb], oacc[ib][jb], 0, 0, 0);
+      }
+      wave_sync();
+    };
     const bool want_marg = A.marg != nullptr;
     const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * ni * L * Q : A.dp, treebytes);
     int8_t* at = A.anc ? A.anc + (size_t)tree * ni * L + site : nullptr;
@@ -583,19 +617,7 @@ __device__ __forceinline__ void mx_body(const MArgs& A, float* lds) {
 #pragma unroll
             for (int t = 0; t < P; ++t) r[t] = valid[t] ? g[t] * __builtin_amdgcn_rcpf(sv[t]) : 0.0f;
             mx_matvec<P>(ktop, lane, r, tv);
-            // outer product: every state j of the site (4 quarters x P)
-#pragma unroll
-            for (int t2 = 0; t2 < P; ++t2) {
-              float uq[4];
-              quarters(u[t2], uq);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const int j = q * P + t2;
-                if (j < kMxMaxQ)
-#pragma unroll
-                  for (int t = 0; t < P; ++t) acc[t][j] = fmaf(r[t], uq[q], acc[t][j]);
-              }
-            }
+            outer(r, u);
             const int crow = desc & 0xFFFF;
 #pragma unroll
             for (int t = 0; t < P; ++t) {
@@ -605,30 +627,17 @@ __device__ __forceinline__ void mx_body(const MArgs& A, float* lds) {
             }
           } else {
             const int code = kind == kKindLeaf ? (int)lleaf[(desc & 0xFFFF) * kMS + s16] : Q;
-            // present state: one-hot weight, acc_i,code += g_i / K_i,code;
-            // missing state / sentinel row (all 1e5): w_ij = K_ij / sum_j K_ij,
-            // acc_ij += g_i / sum_j K_ij for every j
-            float rp[P], rm[P];
+            // present state: one-hot weight w_ij = [j == code]: acc_i,code +=
+            // g_i / K_i,code; missing state / sentinel row (all 1e5): w_ij =
+            // K_ij / sum_j K_ij, acc_ij += g_i / sum_j K_ij for every j
+            float r[P], u[P];
 #pragma unroll
             for (int t = 0; t < P; ++t) {
-              rp[t] = (valid[t] && code < Q) ? g[t] * ik[code * Q + qg * P + t] : 0.0f;
-              rm[t] = (valid[t] && code == Q) ? g[t] * sinv[qg * P + t] : 0.0f;
+              const int st = qg * P + t;
+              r[t] = !valid[t] ? 0.0f : code < Q ? g[t] * ik[code * Q + st] : g[t] * sinv[st];
+              u[t] = (code == Q || st == code) ? 1.0f : 0.0f;
             }
-            const float fc = (float)code;
-#pragma unroll
-            for (int j = 0; j < kMxMaxQ; j += 2) {
-              // one-hot(code == j) = clamp(1 - (code - j)^2), exact for integers
-              const f2 oh = onehot2(pk(fc, fc) - pk((float)j, (float)(j + 1)));
-#pragma unroll
-              for (int t = 0; t < P; ++t) pfma(acc[t][j], acc[t][j + 1], pk(rp[t], rp[t]), oh);
-            }
-            if (__any(active && code == Q)) {
-#pragma unroll
-              for (int j = 0; j < kMxMaxQ; ++j)
-                if (j < Q)
-#pragma unroll
-                  for (int t = 0; t < P; ++t) acc[t][j] += rm[t];
-            }
+            outer(r, u);
           }
         }
       }
@@ -636,23 +645,20 @@ __device__ __forceinline__ void mx_body(const MArgs& A, float* lds) {
       MX_STAMP(9 + (S - 1 - s < 6 ? S - 1 - s : 5));
     }
 
-    // ---- dC partial of the item: the 16 sites of each quarter (DPP row
-    // rotations, lane 16 g keeps the fixed-association total), then the
-    // waves in order through LDS (slots are dead now) ----
+    // ---- dC partial of the item: each wave's blocks (already summed over
+    // the 16 sites by the MFMAs), then the waves in order through LDS (the
+    // slots are dead now) ----
     double* red = reinterpret_cast<double*>(slots);  // [kMW][Q][Q]
     const int Q2 = Q * Q;
 #pragma unroll
-    for (int t = 0; t < P; ++t)
+    for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-      for (int j = 0; j < kMxMaxQ; ++j) {
-        float v = acc[t][j];
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
-        v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
-        const int i = qg * P + t;
-        if (s16 == 0 && valid[t] && j < Q) red[(size_t)wv * Q2 + i * Q + j] = (double)v;
-      }
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = ib * 16 + 4 * (lane >> 4) + q, j = jb * 16 + (lane & 15);
+          if (i < Q && j < Q) red[(size_t)wv * Q2 + i * Q + j] = (double)oacc[ib][jb][q];
+        }
     __syncthreads();
     const int nb = A.B * A.tiles;
     for (int e = threadIdx.x; e < Q2; e += kMW * kWave) {
@@ -701,16 +707,19 @@ int mx_tiles(int L) { return (L + kMS - 1) / kMS; }
 size_t mx_lds_bytes(int ni, int nl, int Q) {
   const int P = (Q + 3) / 4, NB = (P + 3) / 4;
   const size_t b = ((size_t)mx_slot_floats(ni, P, Q) + 2 * NB * P * kWave + (Q + 1) * Q + Q * Q +
-                    kMxMaxQ + 2 * kMxMaxQ * kMxMaxQ) * 4 + (size_t)nl * kMS;
+                    kMxMaxQ + 2 * kMxMaxQ * kMxMaxQ + kMW * 2 * kMS * kXRow) * 4 +
+                   (size_t)nl * kMS;
   return (b + 15) & ~(size_t)15;
 }
 
 // host-side eligibility (everything the host knows; the cost-dependent mode
 // is decided in the kernel): soft, 4 < Q <= 20, the slots fit.  Opt-in
 // (TREX_MX=1) until it beats the state-parallel kernel: measured on C3
-// (tools/mx_check.py, tools/mx_times.py) 170-229 us against 150 us -- the
-// staged workgroup's serial node chain (2 waves per SIMD, LDS-bound to one
-// workgroup per CU) is latency-bound; DESIGN.md section 5.8.
+// (tools/mx_check.py, tools/mx_times.py) 200 us against 150 us (229 us with
+// the earlier VALU outer product, which spilled) -- 148k cycles per
+// workgroup, one workgroup per CU (the D slots alone take 80 KB of LDS), 625
+// tiles = 3 rounds on 256 CUs; the staged node chain is latency-bound at 2
+// waves per SIMD; DESIGN.md section 5.8.
 bool mx_eligible(const WideCall& c) {
   if (!c.soft || c.Q <= 4 || c.Q > kMxMaxQ) return false;
   const char* e = std::getenv("TREX_MX");  // read per call (tests flip it)
