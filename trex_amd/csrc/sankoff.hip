@@ -462,9 +462,9 @@ __device__ __forceinline__ void root_score(const float (&d)[Q][SPT], float a, fl
 // One wave per workgroup = 64*SPT consecutive sites of one tree.  LDS holds
 //   [slots][Q][64][SPT] f32  live D vectors (forward) / cotangents (adjoint)
 //   [nl][64][SPT]       i8   the tile's leaf states (prologue prefetch)
-// Leaf messages take the exact closed form C[i][code] whenever the 1e5
-// sentinel dominates (hard: range(C) < 1e5; soft: exp(-(1e5-range)/tau) <
-// 2^-64), i.e. no transcendental for half of all children.
+// Leaf and sentinel children are lookups in per-code tables (message and
+// adjoint weights; exact closed forms C[i][code] / one-hot when the 1e5
+// sentinel dominates), i.e. no transcendental for half of all children.
 // --------------------------------------------------------------------------
 struct KArgs {
   const int4* steps;
@@ -494,13 +494,25 @@ struct KArgs {
 // row-site offset of the tree's DP rows (lo, hi; x Q floats), 2 spare
 
 
-// LDS map (floats): [0, 64) leaf tables: T[code][i] (message; code Q =
-// missing leaf / all-1e5 sentinel row) at 0, IK[code][i] = 1/K[i][code]
-// (factored-form leaf adjoint weight) at 32; then the slot stack
+// LDS map (floats): [0, 128) leaf tables, one row per leaf code (code Q =
+// missing leaf / all-1e5 sentinel row): T[code][i] = the child's message at
+// 0, W[code][i][j] = its adjoint weight (divided by K_ij in the factored
+// form) at kWTab -- both depend on the code only, so every leaf / sentinel
+// child is a table lookup in both sweeps; then the slot stack
 // [n_slots + 1][64][Q*SPT] (slot n_slots = root cotangent), then the leaf
-// tile [nl][64*SPT] i8 (raw codes, normalised to [0, Q] at use).  The
-// all-1e5 sentinel rows live in registers.
-constexpr int kTabFloats = 64;
+// tile [nl][64*SPT] i8 (raw codes, normalised to [0, Q] at use).
+constexpr int kTabFloats = 128;
+constexpr int kWTab = 32;  // (Q + 1) Q <= 20 message floats precede the weights
+#ifndef TREX_ADJ_RING
+#define TREX_ADJ_RING 2
+#endif
+#ifndef TREX_ADJ_WPE
+#define TREX_ADJ_WPE 5
+#endif
+#ifndef TREX_FWD_WPE
+#define TREX_FWD_WPE 6
+#endif
+constexpr int kAdjRing = TREX_ADJ_RING;  // adjoint DP-row prefetch depth (steps)
 constexpr int kPrefetchRows = 64;  // leaf tiles of <= 64 leaves are prefetched
 
 // Persistent waves: the grid holds as many waves as are co-resident; block
@@ -513,7 +525,7 @@ constexpr int kPrefetchRows = 64;  // leaf tiles of <= 64 leaves are prefetched
 // in LDS, no adjoint re-read, one wave per SIMD -- measured 2.3x slower on the
 // C4 shard and on par for C2; removed in round 3 with the other A/B-only
 // variants)
-template <int Q, int SPT, int MODE, int PHASE, bool LFAST, bool RAGGED>
+template <int Q, int SPT, int MODE, int PHASE, bool RAGGED>
 __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   static_assert(!RAGGED || SPT == 1, "ragged batches use the SPT=1 kernels");
   constexpr bool SOFT = MODE != kHard;
@@ -538,30 +550,60 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   const int kRootSlot = A.n_slots;
   int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT);
 
-  // ---- once per wave: leaf message table T[s][i] = C[i][s], T[Q][i] =
-  // message of an all-1e5 row ----
-  if (lane < Q) {
-    float d1[Q][1], m1[Q][1];
+  // ---- once per wave: the leaf tables.  Lane c <= Q builds row c from the
+  // child row D = (0 at c, 1e5 elsewhere; all 1e5 for c = Q).  When the 1e5
+  // sentinel dominates (hard: range(C) < 1e5; soft: exp(-(1e5 - range)/tau)
+  // < 2^-64) a present leaf's message is exactly C[i][c] and its weights are
+  // one-hot at j = c (x 1/K_ic in the factored form); otherwise (and for the
+  // all-1e5 row) the tables hold the general message / weights of that row,
+  // i.e. what the per-site code computes for it ----
+  {
+    float cmn, cmx;
+    cost_range<Q>(A.cost, cmn, cmx);
+    const float range = cmx - cmn;
+    const bool lfast = (MODE != kHard) ? ((kSentinel - range) * a >= 64.0f) : (range < 99000.0f);
+    if (lane <= Q) {
+      const cptr<float> cost = as_const(A.cost);
+      float d1[Q][1], m1[Q][1], g1[Q][1], w1[Q][Q], gc1[Q][1];
 #pragma unroll
-    for (int j = 0; j < Q; ++j) d1[j][0] = kSentinel;
-    message<Q, 1, MODE>(cf, a, bcoef, d1, m1);
+      for (int j = 0; j < Q; ++j) {
+        d1[j][0] = j == lane ? 0.0f : kSentinel;
+        g1[j][0] = 1.0f;
+      }
 #pragma unroll
-    for (int i = 0; i < Q; ++i)
-      if (i == lane) tab[Q * Q + i] = m1[i][0];
+      for (int i = 0; i < Q; ++i)
 #pragma unroll
-    for (int st_ = 0; st_ < Q; ++st_) {
-      const float cv = as_const(A.cost)[lane * Q + st_];
-      tab[st_ * Q + lane] = cv;
-      if constexpr (MODE == kSoftK) tab[32 + st_ * Q + lane] = fast_exp2((cv - cf.cmin) * a);
+        for (int j = 0; j < Q; ++j) w1[i][j] = 0.0f;
+      if (lfast && lane < Q) {
+#pragma unroll
+        for (int i = 0; i < Q; ++i) {
+          const float cv = cost[i * Q + lane];
+          m1[i][0] = cv;
+          const float ik = MODE == kSoftK ? fast_exp2((cv - cf.cmin) * a) : 1.0f;
+#pragma unroll
+          for (int j = 0; j < Q; ++j) w1[i][j] = j == lane ? ik : 0.0f;
+        }
+      } else {
+        message<Q, 1, MODE>(cf, a, bcoef, d1, m1);
+        message_adjoint<Q, 1, MODE>(cf, a, d1, g1, w1, gc1);
+      }
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        tab[lane * Q + i] = m1[i][0];
+#pragma unroll
+        for (int j = 0; j < Q; ++j) tab[kWTab + (lane * Q + i) * Q + j] = w1[i][j];
+      }
     }
   }
 
   // leaf-tile prefetch: lane l loads dword (l & 15) of rows 4r + (l >> 4),
   // i.e. 16 loads cover 64 leaf rows of a 64-site tile (4-byte aligned rows)
-  // only the forward kernel loops over items: the adjoint's register
-  // footprint is too large to keep a second tile in flight
+  // (all 16 loads in flight together: one HBM round trip per tile, where the
+  // byte-per-lane path waits once per batch of 8 rows).  Only the forward
+  // kernel loops over items and so prefetches the NEXT tile: the adjoint's
+  // register footprint is too large to keep a second tile in flight
   constexpr bool PERSIST = PHASE == 1;
-  const bool pf = !RAGGED && PERSIST && SPT == 1 && (L & 3) == 0 && A.nl <= kPrefetchRows;
+  const bool pf = !RAGGED && SPT == 1 && (L & 3) == 0 && A.nl <= kPrefetchRows;
   const int pf_voff = (lane >> 4) * L + (lane & 15) * 4;
   uint32_t pre[kPrefetchRows / 4];
   auto issue_prefetch = [&](int it) {
@@ -581,7 +623,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
     }
   };
   if (pf) issue_prefetch(item);
-  __syncthreads();  // the table is written by lanes < Q, read by all
+  __syncthreads();  // the tables are written by lanes <= Q, read by all
 
   do {
     // ---- this item's tree: shape and base offsets ----
@@ -617,7 +659,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
     // ---- leaf tile of this item ----
     if (pf) {
       store_prefetch();
-      if (item + stride < item_end) issue_prefetch(item + stride);
+      if (PERSIST && item + stride < item_end) issue_prefetch(item + stride);
     } else {
       const int8_t* lv = A.leaves + leaf_base + sc;
       constexpr int kBatch = 8;
@@ -673,19 +715,12 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
               for (int s = 0; s < SPT; ++s) code[s] = Q;  // all-1e5 row
             }
-            if constexpr (LFAST) {
 #pragma unroll
-              for (int s = 0; s < SPT; ++s) {
-                float r[Q];
-                lds_vec_get<Q>(tab + code[s] * Q, r);
+            for (int s = 0; s < SPT; ++s) {
+              float r[Q];
+              lds_vec_get<Q>(tab + code[s] * Q, r);
 #pragma unroll
-                for (int i = 0; i < Q; ++i) d[c][i][s] = r[i];  // already the message
-              }
-            } else {
-#pragma unroll
-              for (int j = 0; j < Q; ++j)
-#pragma unroll
-                for (int s = 0; s < SPT; ++s) d[c][j][s] = (code[s] == j) ? 0.0f : kSentinel;
+              for (int i = 0; i < Q; ++i) d[c][i][s] = r[i];  // already the message
             }
           }
         }
@@ -693,7 +728,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         for (int c = 0; c < 2; ++c) {
           const int desc = c == 0 ? stp.y : stp.z;
           float m[Q][SPT];
-          if (LFAST && ((desc >> 24) & 3) != kKindInt) {
+          if (((desc >> 24) & 3) != kKindInt) {
 #pragma unroll
             for (int i = 0; i < Q; ++i)
 #pragma unroll
@@ -805,43 +840,26 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         for (int c = 0; c < 2; ++c) {
           const int desc = c == 0 ? stp.y : stp.z;
           const int kind = (desc >> 24) & 3;
-          int code[SPT];
-          bool onehot = false;
-          if (kind == kKindLeaf) {
-            child_code(desc, code);
-            if constexpr (LFAST) {
-              bool miss = false;
+          if (kind != kKindInt) {
+            // leaf / sentinel child: acc_ij += g_i W[code][i][j] (no cotangent)
+            int code[SPT];
+            if (kind == kKindLeaf) {
+              child_code(desc, code);
+            } else {
 #pragma unroll
-              for (int s = 0; s < SPT; ++s) miss |= code[s] == Q;
-              onehot = !__any(miss);
+              for (int s = 0; s < SPT; ++s) code[s] = Q;
             }
-            if (!onehot) {
-#pragma unroll
-              for (int j = 0; j < Q; ++j)
-#pragma unroll
-                for (int s = 0; s < SPT; ++s) cd[c][j][s] = (code[s] == j) ? 0.0f : kSentinel;
-            }
-          } else if (kind != kKindInt) {
-            fill_sentinel<Q, SPT>(cd[c]);
-          }
-          if (onehot) {
-            // exact leaf weights are one-hot: dC[i][code] += g_i
 #pragma unroll
             for (int s = 0; s < SPT; ++s) {
-              float oh[Q], t[Q];
+              float w[Q * Q];
+              lds_vec_get<Q * Q>(tab + kWTab + code[s] * Q * Q, w);
 #pragma unroll
-              for (int j = 0; j < Q; ++j) oh[j] = (code[s] == j) ? 1.0f : 0.0f;
-              if constexpr (MODE == kSoftK) {
-                float ik[Q];
-                lds_vec_get<Q>(tab + 32 + code[s] * Q, ik);
+              for (int i = 0; i < Q; ++i) {
+                float wr[Q];
 #pragma unroll
-                for (int i = 0; i < Q; ++i) t[i] = g[i][s] * ik[i];
-              } else {
-#pragma unroll
-                for (int i = 0; i < Q; ++i) t[i] = g[i][s];
+                for (int j = 0; j < Q; ++j) wr[j] = w[i * Q + j];
+                axpy<Q>(acc[i], g[i][s], wr);
               }
-#pragma unroll
-              for (int i = 0; i < Q; ++i) axpy<Q>(acc[i], t[i], oh);
             }
           } else {
             float gc[Q][SPT];
@@ -867,23 +885,32 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         }
       };
       {
-      float bufA[2][Q][SPT], bufB[2][Q][SPT];
-      I4 sA = load_step(prog, n_int - 1);
-      I4 sB = n_int > 1 ? load_step(prog, n_int - 2) : sA;
+      // ring of kRing row buffers: step k's rows were issued kRing - 1 steps
+      // earlier (more bytes in flight per wave than a ping-pong; the ring is
+      // unrolled so every buffer index is static)
+      constexpr int kRing = kAdjRing;
+      float buf[kRing][2][Q][SPT];
+      I4 sd[kRing];
       const I4 none = {0, 0, 0, 0};  // sentinel children only: prefetch reads nothing
-      prefetch(sA, bufA);
-      for (int k = n_int - 1; k >= 0; k -= 2) {
-        // step k uses A while B fills for step k-1
-        prefetch(k >= 1 ? sB : none, bufB);
-        const I4 cA = sA;
-        if (k >= 2) sA = load_step(prog, k - 2);
-        bstep(cA, bufA);
-        if (k < 1) break;
-        // step k-1 uses B while A fills for step k-2
-        prefetch(k >= 2 ? sA : none, bufA);
-        const I4 cB = sB;
-        if (k >= 3) sB = load_step(prog, k - 3);
-        bstep(cB, bufB);
+#pragma unroll
+      for (int r = 0; r < kRing - 1; ++r) {
+        sd[r] = n_int - 1 - r >= 0 ? load_step(prog, n_int - 1 - r) : none;
+        prefetch(sd[r], buf[r]);
+      }
+      I4 nd = n_int - kRing >= 0 ? load_step(prog, n_int - kRing) : none;
+      for (int k = n_int - 1; k >= 0; k -= kRing) {
+#pragma unroll
+        for (int r = 0; r < kRing; ++r) {
+          // step k - r uses buf[r]; its freed predecessor slot takes the rows
+          // of step k - r - (kRing - 1) (descriptor loaded one round ahead)
+          const int w = (r + kRing - 1) % kRing;
+          const int j = k - r - (kRing - 1);
+          sd[w] = nd;
+          prefetch(sd[w], buf[w]);
+          nd = j - 1 >= 0 ? load_step(prog, j - 1) : none;
+          if (k - r < 0) break;
+          bstep(sd[r], buf[r]);
+        }
       }
       }
 
@@ -915,33 +942,19 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   } while (PERSIST && item < item_end);
 }
 
-template <int Q, int SPT, int MODE, int PHASE, bool RAGGED = false>
-__device__ __forceinline__ void sankoff_dispatch_leaf(const KArgs& A, float* lds) {
-  // leaf messages have the closed form C[i][code] when the 1e5 sentinel
-  // dominates (hard: range(C) < 1e5; soft: exp(-(1e5 - range)/tau) < 2^-64)
-  float cmin, cmax;
-  cost_range<Q>(A.cost, cmin, cmax);
-  const float range = cmax - cmin;
-  const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
-  if (lfast)
-    sankoff_body<Q, SPT, MODE, PHASE, true, RAGGED>(A, lds);
-  else
-    sankoff_body<Q, SPT, MODE, PHASE, false, RAGGED>(A, lds);
-}
-
 template <int Q, int SPT, bool SOFT, int PHASE, bool RAGGED = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? 6 : 5, 8)))
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? TREX_FWD_WPE : TREX_ADJ_WPE, 8)))
 void sankoff_kernel(KArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if constexpr (!SOFT) {
-    sankoff_dispatch_leaf<Q, SPT, kHard, PHASE, RAGGED>(A, lds);
+    sankoff_body<Q, SPT, kHard, PHASE, RAGGED>(A, lds);
   } else {
     float cmin, cmax;
     cost_range<Q>(A.cost, cmin, cmax);
     if (use_ktrick(cmin, cmax, A.a))
-      sankoff_dispatch_leaf<Q, SPT, kSoftK, PHASE, RAGGED>(A, lds);
+      sankoff_body<Q, SPT, kSoftK, PHASE, RAGGED>(A, lds);
     else
-      sankoff_dispatch_leaf<Q, SPT, kSoftDirect, PHASE, RAGGED>(A, lds);
+      sankoff_body<Q, SPT, kSoftDirect, PHASE, RAGGED>(A, lds);
   }
 }
 
@@ -1159,6 +1172,9 @@ int persistent_grid(K kernel, size_t lds, int nitems) {
       if (ncache < 64) cache[ncache++] = Entry{(const void*)kernel, lds, occ};
     }
   }
+#ifdef TREX_FWD_OCC_CAP
+  occ = std::min(occ, TREX_FWD_OCC_CAP);
+#endif
   const long resident = (long)cus * occ / 8 * 8;
   const long want = ((long)nitems + 7) / 8 * 8;
   return (int)std::max(8L, std::min(resident, want));
