@@ -226,7 +226,125 @@ def test_adjacency_roundtrip():
 
 
 def test_abi_version_matches_plan_layout():
-    """trex_version() 5: plans carry the staged program of every tree after
-    the backtrack entries (include/trex_hip.h); a binding that sized v4
-    plans itself must see the bump."""
-    assert lib().trex_version() == 5
+    """trex_version() 6: plans carry the lane-per-site program of every tree
+    after the staged programs, and info[0] packs its slot count above the
+    stack depth (include/trex_hip.h); a binding that sized v5 plans itself
+    must see the bump."""
+    assert lib().trex_version() == 6
+    ch = balanced_children(64, B=1)
+    p = TreePlan(ch)
+    assert p.n_slots == 5 and p.lane_slots == 12 and p.slot_word == 5 | (13 << 16)
+
+
+def _lanes(plan, b):
+    """Decode tree b's lane-per-site region (trex_common.h)."""
+    from trex_amd._lib import TREX_PLAN_HEADER_INTS
+
+    ni, W = plan.n_int, STAGE_WAVES
+    staged = 4 * ni + ((ni * W + 2 + 3) & ~3)
+    steps_off = 8 + ((ni + 1 + 3) & ~3)
+    stride = steps_off + 4 * ni
+    base = TREX_PLAN_HEADER_INTS + plan.B * ni * 6 + plan.B * staged + b * stride
+    r = plan.host[base:base + stride]
+    S, n_slots, n_steps, n_inl = (int(x) for x in r[:4])
+    offs = r[4:5 + S]
+    steps = r[steps_off:steps_off + 4 * n_steps].reshape(n_steps, 4)
+    inl = r[steps_off + 4 * n_steps:steps_off + 4 * (n_steps + n_inl)].reshape(n_inl, 4)
+    return S, n_slots, offs, steps, inl
+
+
+@pytest.mark.parametrize("kind", ["random", "balanced", "fwdref", "dag", "cycle", "small"])
+def test_lane_program_reproduces_oracle(kind):
+    """The lane-per-site program of sankoff_site.hip, executed stage by stage
+    with an LDS-slot model: every internal row is computed exactly once
+    (task or inline), a task's task children finish in earlier stages, no
+    slot is overwritten while live (forward D, then adjoint cotangent over
+    the same interval), and the D of every row equals the oracle DP table.
+    Trees with a shared child or an unreached row have no program."""
+    if kind == "random":
+        ch = random_topologies(4, 40, seed=1)
+    elif kind == "balanced":
+        ch = balanced_children(64, B=2)
+    elif kind == "small":
+        ch = balanced_children(2, B=1)
+    else:
+        ch = weird_children(kind)[None]
+    plan = TreePlan(ch)
+    n_all = ch.shape[1]
+    nl = (n_all + 1) // 2
+    ni = n_all - nl
+    L, Q = 11, 4
+    leaves = random_leaves(ch.shape[0], nl, L, Q, seed=2, missing=0.1)
+    cost = int_cost(Q, seed=3).astype(np.float64)
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, 0.0)
+    for b in range(ch.shape[0]):
+        S, n_slots, offs, steps, inl = _lanes(plan, b)
+        if n_slots < 0:
+            assert plan.n_dag_nodes or plan.n_unreached or kind in ("dag", "cycle", "fwdref")
+            assert plan.lane_slots == -1
+            continue
+        lD = leaf_dp(leaves[b], Q)
+        dp = np.full((ni, L, Q), np.nan)
+        slot_val = {}   # slot -> row currently held
+        done = set()
+
+        def msg(D):
+            return (cost[None] + D[:, None, :]).min(axis=2)
+
+        def leafish(d):
+            k = (d >> 24) & 3
+            assert k in (0, 1)
+            return lD[d & 0xFFFF] if k == 1 else np.full((L, Q), SENTINEL)
+
+        def inline_d(idx, depth=0):
+            row, da, db, h = (int(x) for x in inl[idx])
+            acc = 0
+            for d in (da, db):
+                if (d >> 24) & 3 == 3:
+                    assert depth == 0 and h == 2
+                    acc = acc + msg(inline_d(d & 0xFFFF, 1))
+                else:
+                    acc = acc + msg(leafish(d))
+            dp[row] = acc
+            done.add(row)
+            return dp[row]
+
+        for s in range(S):
+            for k in range(offs[s], offs[s + 1]):
+                w0, da, db, flags = (int(x) for x in steps[k])
+                row, sl = w0 & 0xFFFF, (w0 >> 16) & 0xFF
+                acc = 0
+                for d in (da, db):
+                    kd = (d >> 24) & 3
+                    if kd == 2:
+                        c, cs = d & 0xFFFF, (d >> 16) & 0xFF
+                        assert slot_val.get(cs) == c, "task child not in its slot"
+                        acc = acc + msg(dp[c])
+                    elif kd == 3:
+                        acc = acc + msg(inline_d(d & 0xFFFF))
+                    else:
+                        acc = acc + msg(leafish(d))
+                dp[row] = acc
+                assert row not in done
+                done.add(row)
+                if flags & 1:
+                    assert row == ni - 1 and s == S - 1 and offs[s + 1] - offs[s] == 1
+                assert 0 <= sl < n_slots
+                slot_val[sl] = row  # overwrites only dead rows (checked by the reads above)
+        assert done == set(range(ni))
+        np.testing.assert_array_equal(dp.transpose(0, 2, 1), ref["dp"][b])
+        # adjoint: the same intervals in reverse -- a task's cotangent is written
+        # into its slot at its parent's stage and read at its own stage
+        holder = {}
+        for s in reversed(range(S)):
+            for k in range(offs[s], offs[s + 1]):
+                w0, da, db, flags = (int(x) for x in steps[k])
+                row, sl = w0 & 0xFFFF, (w0 >> 16) & 0xFF
+                if flags & 1:
+                    holder[sl] = row  # the root's cotangent, written at the adjoint's start
+                assert holder.get(sl) == row, "cotangent slot overwritten before its read"
+                for d in (da, db):
+                    if (d >> 24) & 3 == 2:
+                        holder[(d >> 16) & 0xFF] = d & 0xFFFF
+    if kind == "balanced":
+        assert plan.lane_slots == 12

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <functional>
 #include <queue>
 #include <set>
 #include <vector>
@@ -333,6 +334,104 @@ void stage_one_tree(const int32_t* ch, int n_all, int32_t* region) {
   }
 }
 
+// Lane-per-site program of one tree (layout: trex_common.h).  Internal rows
+// of height <= 2 (height: 1 + the tallest internal child; leaves and 1e5
+// rows 0) are computed inline by the task that consumes them; every other
+// row (and the root) is a task.  A task's stage is its height - 3 (the
+// root's at least 0), so a stage depends only on earlier stages.  A task
+// row's LDS slot holds its D from its own stage to its parent's (the root's:
+// its own stage), then, in the reversed adjoint, its cotangent over the same
+// interval: slots are
+// interval-coloured, reused once the interval has ended.  Returns the slot
+// count, or -1 when the tree cannot run this program (a shared internal
+// child -- trex's DAG quirk --, an internal row the root does not reach, or
+// more than 255 slots); the other kernels then serve the batch.
+int lane_program_one_tree(const int32_t* ch, int n_all, int32_t* region) {
+  const int nl = (n_all + 1) / 2;
+  const int ni = n_all - nl;
+  std::memset(region, 0, sizeof(int32_t) * lp_tree_ints(ni));
+  region[1] = -1;
+  std::vector<int> kind(2 * ni), idx(2 * ni), refs(ni, 0), height(ni, 1), parent(ni, -1);
+  for (int r = 0; r < ni; ++r) {
+    const int node = nl + r;
+    for (int k = 0; k < 2; ++k) {
+      const int c = ch[2 * node + k];  // validated by plan_one_tree
+      if (c == -1 || c >= node) {
+        kind[2 * r + k] = kKindSent;
+        idx[2 * r + k] = 0;
+      } else if (c < nl) {
+        kind[2 * r + k] = kKindLeaf;
+        idx[2 * r + k] = c;
+      } else {
+        kind[2 * r + k] = kKindInt;
+        idx[2 * r + k] = c - nl;
+        refs[c - nl] += 1;
+        parent[c - nl] = r;
+        height[r] = std::max(height[r], height[c - nl] + 1);
+      }
+    }
+  }
+  const int root = ni - 1;
+  for (int r = 0; r < ni; ++r)
+    if (refs[r] > 1 || (r != root && refs[r] == 0)) return -1;  // DAG / unreached row
+  std::vector<char> task(ni, 0);
+  std::vector<int> stage(ni, 0);
+  int S = 1;
+  for (int r = 0; r < ni; ++r) {
+    task[r] = r == root || height[r] >= 3;
+    stage[r] = std::max(0, height[r] - 3);
+    if (task[r]) S = std::max(S, stage[r] + 1);
+  }
+  // slots: interval colouring over [stage(r), stage(parent(r))]
+  std::vector<int> order;
+  for (int r = 0; r < ni; ++r)
+    if (task[r]) order.push_back(r);
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return stage[x] < stage[y]; });
+  std::vector<int> slot(ni, 0xFF), slot_end;
+  for (int r : order) {
+    const int st = stage[r], en = r == root ? stage[r] : stage[parent[r]];
+    int s = 0;
+    while (s < (int)slot_end.size() && slot_end[s] >= st) ++s;
+    if (s == (int)slot_end.size()) slot_end.push_back(en);
+    else slot_end[s] = en;
+    slot[r] = s;
+  }
+  const int n_slots = (int)slot_end.size();
+  if (n_slots > 255) return -1;
+  // inline rows in post-order of their task (children first): index list
+  std::vector<int> inl(ni, -1);
+  std::vector<int32_t> ient;
+  std::function<int32_t(int, int)> desc = [&](int r, int k) -> int32_t {
+    const int kd = kind[2 * r + k], c = idx[2 * r + k];
+    if (kd == kKindSent) return 0;
+    if (kd == kKindLeaf) return (c & 0xFFFF) | (kKindLeaf << 24);
+    if (task[c]) return (c & 0xFFFF) | (slot[c] << 16) | (kKindInt << 24);
+    const int32_t d0 = desc(c, 0), d1 = desc(c, 1);
+    inl[c] = (int)(ient.size() / 4);
+    ient.insert(ient.end(), {c, d0, d1, height[c]});
+    return (inl[c] & 0xFFFF) | (kKindInline << 24);
+  };
+  const int n_steps = (int)order.size();
+  int32_t* offs = region + 4;
+  int32_t* steps = region + lp_steps_offset(ni);
+  for (int s = 0; s <= S; ++s) offs[s] = n_steps;
+  for (int k = n_steps - 1; k >= 0; --k) offs[stage[order[k]]] = k;
+  for (int s = S - 1; s >= 0; --s) offs[s] = std::min(offs[s], offs[s + 1]);
+  for (int k = 0; k < n_steps; ++k) {
+    const int r = order[k];
+    steps[4 * k] = (r & 0xFFFF) | (slot[r] << 16);
+    steps[4 * k + 1] = desc(r, 0);
+    steps[4 * k + 2] = desc(r, 1);
+    steps[4 * k + 3] = r == root ? kStepRoot : 0;
+  }
+  if (!ient.empty()) std::memcpy(steps + 4LL * n_steps, ient.data(), ient.size() * sizeof(int32_t));
+  region[0] = S;
+  region[1] = n_slots;
+  region[2] = n_steps;
+  region[3] = (int)(ient.size() / 4);
+  return n_slots;
+}
+
 }  // namespace
 
 }  // namespace trex
@@ -340,7 +439,8 @@ void stage_one_tree(const int32_t* ch, int n_all, int32_t* region) {
 extern "C" int64_t trex_plan_ints(int B, int n_all) {
   if (B <= 0 || n_all < 2) return 0;
   const int ni = n_all - (n_all + 1) / 2;
-  return TREX_PLAN_HEADER_INTS + (int64_t)B * ni * 6 + (int64_t)B * trex::staged_tree_ints(ni);
+  return TREX_PLAN_HEADER_INTS + (int64_t)B * ni * 6 +
+         (int64_t)B * (trex::staged_tree_ints(ni) + trex::lp_tree_ints(ni));
 }
 
 extern "C" int trex_plan_build(const int32_t* children, int B, int n_all,
@@ -354,13 +454,17 @@ extern "C" int trex_plan_build(const int32_t* children, int B, int n_all,
   int32_t* fwd = plan + TREX_PLAN_HEADER_INTS;
   int32_t* bt = fwd + (int64_t)B * ni * 4;
   int32_t* staged = bt + (int64_t)B * ni * 2;
-  int max_slots = 0, all_bt_ok = 1, dag = 0, unr = 0;
+  int32_t* lanes = staged + (int64_t)B * staged_tree_ints(ni);
+  int max_slots = 0, all_bt_ok = 1, dag = 0, unr = 0, lp_slots = 0;
   for (int b = 0; b < B; ++b) {
     int s = 0, ok = 0, d = 0, u = 0;
     if (!plan_one_tree(children + (int64_t)b * n_all * 2, n_all, fwd + (int64_t)b * ni * 4,
                        bt + (int64_t)b * ni * 2, &s, &ok, &d, &u))
       return set_error(TREX_E_TOPOLOGY, "trex_plan_build: tree %d has an invalid child list", b);
     stage_one_tree(children + (int64_t)b * n_all * 2, n_all, staged + b * staged_tree_ints(ni));
+    const int ls = lane_program_one_tree(children + (int64_t)b * n_all * 2, n_all,
+                                         lanes + b * lp_tree_ints(ni));
+    lp_slots = (ls < 0 || lp_slots < 0) ? -1 : std::max(lp_slots, ls);
     max_slots = std::max(max_slots, s);
     all_bt_ok &= ok;
     dag += d;
@@ -373,8 +477,11 @@ extern "C" int trex_plan_build(const int32_t* children, int B, int n_all,
   plan[4] = ni;
   plan[5] = max_slots;
   plan[6] = all_bt_ok;
+  plan[7] = lp_slots;
   if (info) {
-    info[0] = max_slots;
+    // low 16 bits: the stack depth; bits 16-23: lane-program slots + 1 (0: a
+    // tree of the batch cannot run the lane-per-site kernel)
+    info[0] = max_slots | ((lp_slots < 0 ? 0 : lp_slots + 1) << 16);
     info[1] = all_bt_ok;
     info[2] = dag;
     info[3] = unr;

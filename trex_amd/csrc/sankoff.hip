@@ -1265,7 +1265,11 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
     return set_error(TREX_E_ARG, "%s: tau must be finite and >= 0 (got %g)", fn, tau);
   if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
-  if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  if (n_slots < 0) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  // plan info[0]: stack depth | (lane-program slots + 1) << 16
+  const int lp_slots = ((n_slots >> 16) & 0xFF) - 1;
+  n_slots &= 0xFFFF;
+  if (n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
   if (Q > 4 || wide_small_q(B, L, Q)) {
     WideCall c;
     c.phase = phase;
@@ -1291,7 +1295,18 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
     c.workspace = workspace;
     c.stream = stream;
     const int32_t* staged = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 6;
-    if (mx_eligible(c)) {
+    const int32_t* lanes = staged + (int64_t)B * staged_tree_ints(s.ni);
+    if (site_eligible(c, lp_slots)) {
+      // the lane-per-site kernel first (sankoff_site.hip): its prologue
+      // kernel decides the mode on the device and writes a flag (tail of the
+      // workspace) the state-parallel launch below checks
+      char* tail = static_cast<char*>(workspace) + wide_workspace_bytes(B, L, Q);
+      int* flag = reinterpret_cast<int*>(tail - 128);
+      float* kg = reinterpret_cast<float*>(tail - 3456);  // K and K^T
+      if (int e = site_run(fn, c, lanes, lp_slots, flag, kg)) return e;
+      c.mx_flag = flag;
+      c.mx_tiles = site_tiles(L);
+    } else if (mx_eligible(c)) {
       // the matrix-core kernel first (sankoff_mx.hip); its device flag (a
       // word in the workspace's tail slack) tells the state-parallel launch
       // below whether to run
@@ -1369,7 +1384,7 @@ using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 5; }
+extern "C" int trex_version(void) { return 6; }
 
 extern "C" int trex_dp_site_major(int Q) {
   (void)Q;

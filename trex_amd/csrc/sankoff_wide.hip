@@ -424,6 +424,56 @@ __global__ __launch_bounds__(kReduceThreads) void wide_reduce_kernel(const doubl
   if (threadIdx.x == 0) *dst = (float)v;
 }
 
+// Two-level form of the same fixed-order reduction for large uniform grids
+// (C4: 80 896 items per dC entry, where one 1 024-thread block per entry is a
+// chain of ten dependent load rounds, 23 us).  Stage 1: blocks [0, Q2 * P)
+// each sum one kChunk-item chunk of one dC entry and write the result IN
+// PLACE over the chunk's first partial (only this block reads the chunk);
+// the remaining blocks sum tree scores, one wave per tree.  Stage 2: one wave
+// per dC entry sums its P chunk results.  Partials are rewritten by every
+// Sankoff launch, so consuming them in place is safe.
+constexpr int kChunk = 2048;
+#ifndef TREX_REDUCE2_MIN  // items per dC entry above which the two-level form runs
+#define TREX_REDUCE2_MIN (4 * kChunk)
+#endif
+constexpr int kStage1Threads = 256;
+__global__ __launch_bounds__(kStage1Threads) void reduce_stage1_kernel(
+    const double* __restrict__ part_tree, double* __restrict__ part_dc, int B, int tiles, int ndc,
+    int P, int do_tree, float* __restrict__ tree_score) {
+  __shared__ double red[kStage1Threads];
+  const int b = blockIdx.x;
+  const size_t nb = (size_t)B * tiles;
+  if (b < ndc) {
+    const int q = b / P, p = b - q * P;
+    double* src = part_dc + (size_t)q * nb + (size_t)p * kChunk;
+    const int n = (int)min((size_t)kChunk, nb - (size_t)p * kChunk);
+    const double v = fixed_sum<kStage1Threads>(src, n, red, threadIdx.x);
+    if (threadIdx.x == 0) *src = v;  // every thread's loads retired before fixed_sum's barriers
+    return;
+  }
+  if (!do_tree) return;
+  const int t = (b - ndc) * (kStage1Threads / kWave) + (int)(threadIdx.x / kWave);
+  if (t >= B) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const double* src = part_tree + (size_t)t * tiles;
+  double acc = 0.0;
+  for (int k = lane; k < tiles; k += kWave) acc += src[k];
+  acc = wave_sum_lane0(acc);
+  if (lane == 0) tree_score[t] = (float)acc;
+}
+
+__global__ __launch_bounds__(kWave) void reduce_stage2_kernel(const double* __restrict__ part_dc,
+                                                               int B, int tiles, int P,
+                                                               float* __restrict__ d_cost) {
+  const int q = blockIdx.x;
+  const int lane = threadIdx.x;
+  const double* src = part_dc + (size_t)q * ((size_t)B * tiles);
+  double acc = 0.0;
+  for (int p = lane; p < P; p += kWave) acc += src[(size_t)p * kChunk];
+  acc = wave_sum_lane0(acc);
+  if (lane == 0) d_cost[q] = (float)acc;
+}
+
 // trex-exact ancestral reconstruction on the site-major table
 // (sankoff.py:166-185, 191-267): one lane per site, C in LDS
 // trex-exact reconstruction for Q > 4 (sankoff.py:166-185, 191-267): one
@@ -682,7 +732,9 @@ size_t wide_lds_bytes(int n_slots, int nl, int ni, int Q) {
 
 int64_t wide_workspace_bytes(int B, int L, int Q) {
   const int64_t nb = (int64_t)B * wide_tiles(L, Q);
-  return nb * 8 * (1 + (int64_t)Q * Q) + 256;
+  // tail: staged-kernel counter (128 B) | K and K^T for the lane-per-site
+  // kernel (3.25 KB, sankoff_site.hip) | mode flag (128 B)
+  return nb * 8 * (1 + (int64_t)Q * Q) + 3584;
 }
 
 int wide_run(const char* fn, const WideCall& c) {
@@ -796,6 +848,20 @@ int partial_reduce(const char* fn, const double* part_tree, const double* part_d
                    const int* mx_flag, int mx_tiles) {
   const bool do_tree = (phase & 1) != 0;
   const bool do_dc = (phase & 2) != 0;
+  const int64_t nb = (int64_t)B * tiles;
+  if (!first && !mx_flag && do_dc && nb > TREX_REDUCE2_MIN) {
+    const int P = (int)((nb + kChunk - 1) / kChunk);
+    const int ndc = Q * Q * P;
+    const int tblocks = do_tree ? (B + kStage1Threads / kWave - 1) / (kStage1Threads / kWave) : 0;
+    hipLaunchKernelGGL(reduce_stage1_kernel, dim3(ndc + tblocks), dim3(kStage1Threads), 0,
+                       (hipStream_t)stream, part_tree, const_cast<double*>(part_dc), B, tiles, ndc,
+                       P, do_tree ? 1 : 0, tree_score);
+    hipLaunchKernelGGL(reduce_stage2_kernel, dim3(Q * Q), dim3(kWave), 0, (hipStream_t)stream,
+                       part_dc, B, tiles, P, d_cost);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+    return TREX_OK;
+  }
   const int rgrid = (do_tree ? B : 0) + (do_dc ? Q * Q : 0);
   hipLaunchKernelGGL(wide_reduce_kernel, dim3(rgrid), dim3(kReduceThreads), 0, (hipStream_t)stream,
                      part_tree, part_dc, B, tiles, Q * Q, do_tree ? 1 : 0, tree_score, d_cost,

@@ -36,6 +36,19 @@ inline int64_t staged_tree_ints(int ni) {
   return 4LL * ni + (((int64_t)ni * kStageWaves + 2 + 3) & ~3LL);
 }
 
+// Lane-per-site program (sankoff_site.hip), after the staged regions: one
+// region of lp_tree_ints(ni) ints per tree (plan.cpp lane_program_one_tree):
+//   [0] S (stages)  [1] n_slots (-1: the tree cannot run it)  [2] n_steps
+//   [3] n_inline  [4 .. 4 + S] stage offsets: stage s = steps [off[s], off[s+1])
+//   steps at lp_steps_offset(ni): [n_steps][4] = {row | slot << 16,
+//     child desc 0, child desc 1, flags (kStepRoot)}, then the inline rows
+//     [n_inline][4] = {row, child desc 0, child desc 1, height}, children first.
+//   child desc: kind << 24 | (sentinel: 0; leaf: leaf index; task row:
+//     row | slot << 16 (kKindInt); inline row: its index (kKindInline))
+constexpr int kKindInline = 3;
+inline int64_t lp_steps_offset(int ni) { return 8 + (((int64_t)ni + 1 + 3) & ~3LL); }
+inline int64_t lp_tree_ints(int ni) { return lp_steps_offset(ni) + 4LL * ni; }
+
 // backtrack entry kinds (bits 16-19 of word 0)
 constexpr int kBtRoot = 0;
 constexpr int kBtReal = 1;
@@ -121,6 +134,11 @@ bool mx_eligible(const WideCall& c);
 int mx_tiles(int L);
 size_t mx_lds_bytes(int ni, int nl, int Q);
 int mx_run(const char* fn, const WideCall& c, const int32_t* staged, int* flag);
+// lane-per-site kernel for the factored softmin, 4 < Q <= 20 (sankoff_site.hip)
+bool site_eligible(const WideCall& c, int lp_slots);
+int site_tiles(int L);
+int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots, int* flag,
+             float* kg);
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream);
 int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,

@@ -138,7 +138,7 @@ class SankoffEngine:
             ts = torch.empty((p.B,), dtype=torch.float32, device=self.device)
         flags = TREX_FLAG_HARD_ROOT if hard_root else 0
         check(lib().trex_sankoff_fwd(
-            ptr(self.plan_dev), p.n_slots, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
+            ptr(self.plan_dev), p.slot_word, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
             self.Q, float(tau), flags, ptr(dp_t), ptr(ss), ptr(ts), ptr(self.workspace),
             self.workspace.numel(), stream_handle(self.device)))
         return ForwardResult(ts, dp_t, ss)
@@ -170,7 +170,7 @@ class SankoffEngine:
                 raise ValueError("d_tree_score must be (B,)")
         flags = TREX_FLAG_HARD_ROOT if hard_root else 0
         check(lib().trex_sankoff_bwd(
-            ptr(self.plan_dev), p.n_slots, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
+            ptr(self.plan_dev), p.slot_word, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
             self.Q, float(tau), flags, ptr(dp), ptr(d_tree_score), ptr(dc), ptr(mg), ptr(an),
             ptr(self.workspace), self.workspace.numel(), stream_handle(self.device)))
         return dc, mg, an
@@ -207,7 +207,7 @@ class SankoffEngine:
                 raise ValueError("d_tree_score must be (B,)")
         flags = TREX_FLAG_HARD_ROOT if hard_root else 0
         check(lib().trex_sankoff_fwd_bwd(
-            ptr(self.plan_dev), p.n_slots, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
+            ptr(self.plan_dev), p.slot_word, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
             self.Q, float(tau), flags, ptr(dp_t), ptr(ss), ptr(ts), ptr(d_tree_score), ptr(dc),
             ptr(mg), ptr(an), ptr(self.workspace), self.workspace.numel(),
             stream_handle(self.device)))

@@ -108,7 +108,11 @@ class TreePlan:
         check(L.trex_plan_build(ch.ctypes.data, self.B, self.n_all, self.host.ctypes.data,
                                 info.ctypes.data))
         self.children = ch
-        self.n_slots = int(info[0])
+        # info[0]: stack depth | (lane-program slots + 1) << 16; the C calls
+        # take the whole word
+        self.slot_word = int(info[0])
+        self.n_slots = self.slot_word & 0xFFFF
+        self.lane_slots = ((self.slot_word >> 16) & 0xFF) - 1
         self.backtrack_ok = int(info[1])
         self.n_dag_nodes = int(info[2])
         self.n_unreached = int(info[3])
