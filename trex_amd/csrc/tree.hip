@@ -524,13 +524,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
   const int lofs = r * kG3Stride + 16 * h;
   auto compute = [&](const unsigned char* buf) {
-    int a = a0, b = b0;
+    int a = a0, b = b0, ap = -1;
+    h8 ah, al;
 #pragma unroll
     for (int t = 0; t < kG3Tiles; ++t) {
-      const unsigned char* pa = buf + a * (32 * kG3Stride) + lofs;
+      // the A fragment only when the row strip changes (a wave's 13 tiles
+      // span 2-3 strips): LDS read bytes per chunk 416 -> ~240 KB per CU
+      if (a != ap) {
+        const unsigned char* pa = buf + a * (32 * kG3Stride) + lofs;
+        ah = *reinterpret_cast<const h8*>(pa);
+        al = *reinterpret_cast<const h8*>(pa + 32);
+        ap = a;
+      }
       const unsigned char* pb = buf + b * (32 * kG3Stride) + lofs;
-      const h8 ah = *reinterpret_cast<const h8*>(pa);
-      const h8 al = *reinterpret_cast<const h8*>(pa + 32);
       const h8 bh = *reinterpret_cast<const h8*>(pb);
       const h8 bl = *reinterpret_cast<const h8*>(pb + 32);
       acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
