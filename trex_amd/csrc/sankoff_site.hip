@@ -385,14 +385,35 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
   if constexpr (FWD) {
     for (int s = 0; s < S; ++s) {
       const int lo = pword(4 + s), hi = pword(5 + s);
-      for (int k = lo + wv; k < hi; k += kSWv) {
-        const I4 stp = load_step(steps, k);
-        float dv[kSQ];
-        child_add(stp.y, dv, true, true);
-        child_add(stp.z, dv, false, true);
-        const int row = stp.x & 0xFFFF;
-        store_row(rdp, row, dv);
-        slot_put((stp.x >> 16) & 0xFF, dv);
+      // a stage of at most kSWv / 2 tasks runs one child per wave (items =
+      // task x child): the c = 1 wave hands its message over through its
+      // scratch column after a barrier, the c = 0 wave adds it (m0 + m1, the
+      // one-wave order) and writes the row
+      const bool split = 2 * (hi - lo) <= kSWv;
+      const int nit = split ? 2 * (hi - lo) : hi - lo;
+      I4 stp = I4{0, 0, 0, 0};
+      float dv[kSQ];
+      for (int it = wv; it < nit; it += kSWv) {
+        stp = load_step(steps, lo + (split ? it >> 1 : it));
+        const int c_lo = split ? (it & 1) : 0, c_hi = split ? c_lo + 1 : 2;
+        for (int c = c_lo; c < c_hi; ++c) child_add(c == 0 ? stp.y : stp.z, dv, c == c_lo, true);
+        if (split && c_lo == 1) {
+#pragma unroll
+          for (int i = 0; i < kSQ; ++i) xr[i * kWave + lane] = dv[i];
+        } else if (!split) {
+          store_row(rdp, stp.x & 0xFFFF, dv);
+          slot_put((stp.x >> 16) & 0xFF, dv);
+        }
+      }
+      if (split) {
+        site_barrier();
+        if (wv < nit && (wv & 1) == 0) {
+          const float* px = scr + (size_t)(wv + 1) * 2 * kSlotF;
+#pragma unroll
+          for (int i = 0; i < kSQ; ++i) dv[i] = dv[i] + px[i * kWave + lane];
+          store_row(rdp, stp.x & 0xFFFF, dv);
+          slot_put((stp.x >> 16) & 0xFF, dv);
+        }
       }
       site_barrier();
       SITE_STAMP(2 + (s < 5 ? s : 5));
@@ -635,10 +656,8 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
                   ((e.z >> 24) & 3) == kKindInline ? (int)0x7F000000 : e.z);
     };
 
-    for (int s = S - 1; s >= 0; --s) {
-      const int lo = pword(4 + s), hi = pword(5 + s);
-      for (int k = lo + wv; k < hi; k += kSWv) {
-        const I4 stp = load_step(steps, k);
+    // children c in [c_lo, c_hi) of task row stp
+    auto adj_task = [&](const I4& stp, int c_lo, int c_hi) {
         const int vslot = (stp.x >> 16) & 0xFF;
         int lf0 = 0x7F000000, lf1 = 0x7F000000;  // leaf / 1e5 children (kind 3 marks none)
         // one child at a time: its D row (task rows, height-2 inline rows:
@@ -647,6 +666,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         // child's subtree)
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
+          if (c < c_lo || c >= c_hi) continue;
           const int desc = c == 0 ? stp.y : stp.z;
           const int kind = (desc >> 24) & 3;
           if (kind == kKindInt || kind == kKindInline) {
@@ -672,9 +692,22 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
             lf1 = desc;
           }
         }
-        float g[kSQ];
-        slot_get(vslot, g);
-        leafish_adj(g, lf0, lf1);
+        if (lf0 != 0x7F000000 || lf1 != 0x7F000000) {
+          float g[kSQ];
+          slot_get(vslot, g);
+          leafish_adj(g, lf0, lf1);
+        }
+    };
+    for (int s = S - 1; s >= 0; --s) {
+      const int lo = pword(4 + s), hi = pword(5 + s);
+      // a stage of at most kSWv / 2 tasks: one child per wave (the two
+      // children's adjoints are independent: distinct slots, per-wave dC
+      // accumulators; the c = 0 item emits the parent row)
+      const bool split = 2 * (hi - lo) <= kSWv;
+      const int nit = split ? 2 * (hi - lo) : hi - lo;
+      for (int it = wv; it < nit; it += kSWv) {
+        const int c_lo = split ? (it & 1) : 0;
+        adj_task(load_step(steps, lo + (split ? it >> 1 : it)), c_lo, split ? c_lo + 1 : 2);
       }
       site_barrier();
       SITE_STAMP(10 + (S - 1 - s < 5 ? S - 1 - s : 5));
