@@ -391,8 +391,13 @@ def c5_gemm_kernels(torch, opt):
     if opt.gemm == "x3":
         gram = lambda: check(L_.trex_tree_gram_skip_x3(ptr(opt.S), N, K, opt.skip_rows, 1.0,  # noqa: E731
                                                        ptr(opt.G), ptr(opt.ws), opt.ws.numel(), st))
-        mf = lambda: check(L_.trex_tree_mf_rows_x3(ptr(opt.M), ptr(opt.S), N, K, nl, na,  # noqa: E731
-                                                   float(N + 1), 1.0, ptr(dS), st))
+        if opt.codes is not None:  # the step's own MF: leaf rows read as codes
+            mf = lambda: check(L_.trex_tree_mf_rows_x3_codes(  # noqa: E731
+                ptr(opt.M), ptr(opt.S), N, K, nl, na, float(N + 1), 1.0, ptr(opt.codes), nl,
+                ptr(dS), st))
+        else:
+            mf = lambda: check(L_.trex_tree_mf_rows_x3(ptr(opt.M), ptr(opt.S), N, K, nl, na,  # noqa: E731
+                                                       float(N + 1), 1.0, ptr(dS), st))
     else:
         gram = lambda: check(L_.trex_tree_gram_skip(ptr(opt.S), N, K, opt.skip_rows, ptr(opt.G),  # noqa: E731
                                                     ptr(opt.ws), opt.ws.numel(), st))
@@ -412,9 +417,12 @@ def c5_gemm_kernels(torch, opt):
     out = {}
     nt, sk = (N + 31) // 32, opt.skip_rows // 32
     tiles = nt * (nt + 1) // 2 - sk * (sk + 1) // 2
+    # MF operand bytes: the code rows as one byte per site (leaf codes) or f32 rows
+    lcr = int(L_.trex_tree_leaf_code_rows(nl)) if opt.codes is not None else 0
+    s_mf = (N - lcr) * K * 4 + lcr * (K // opt.Q)
     for name, fn, abytes, flops in (
             ("gram", gram, N * K * 4 + N * N * 4, tiles * 32 * 32 * K * 2),
-            ("mf", mf, N * K * 4 + N * N * 4 + na * K * 4, ((na + 31) // 32 * 32) * nt * 32 * K * 2)):
+            ("mf", mf, s_mf + N * N * 4 + na * K * 4, ((na + 31) // 32 * 32) * nt * 32 * K * 2)):
         sec = timed(fn)
         d = {"us": round(sec * 1e6, 2), "algorithmic_bytes": abytes,
              "GBs": round(abytes / sec / 1e9, 1), "hbm_frac": round(abytes / sec / 1e9 / HBM_PEAK_GBS, 4)}
@@ -440,6 +448,7 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3"):
     sites shard: one all-reduce of the 511 x 511 Gram per step
     (strong scaling: the 50 000 sites are split).  Eager launches (Adam's bias
     correction changes every step)."""
+    from trex_amd._lib import lib
     from trex_amd.datagen import generate_groundtruth
     from trex_amd.distributed import shard_bounds
     from trex_amd.tree import TreeOptimizer, gumbel_noise
@@ -486,7 +495,8 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3"):
     # / moments, writes logits / moments and the next step's S rows
     Kl = (hi - lo) * Q
     na = nl - 1
-    step_bytes = n * Kl * 4 + (n * Kl * 4 + na * Kl * 4) + na * Kl * 4 * 8
+    lcr = int(lib().trex_tree_leaf_code_rows(nl)) if opt.codes is not None else 0
+    step_bytes = n * Kl * 4 + ((n - lcr) * Kl * 4 + lcr * (hi - lo) + na * Kl * 4) + na * Kl * 4 * 8
     gemm_desc = ("f16x3 split-product MFMA GEMMs (f32 accumulate; rtol 1e-5 vs fp64 at this "
                  "size, tests/test_configs_full_gpu.py)" if opt.gemm == "x3" else "f32 MFMA GEMMs")
     res = {"workload": "C5: 511-node relaxed tree x 50000 sites x 4 states, joint Adam step "
@@ -495,7 +505,7 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3"):
                           else ""),
            "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec, "n_gpus": world,
            "scaling": "strong" if world > 1 else None, "loss_last": float(loss),
-           "gemm": opt.gemm,
+           "gemm": opt.gemm, "leaf_codes": opt.codes is not None,
            "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": step_bytes,
                         "achieved": round(step_bytes / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(step_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}}

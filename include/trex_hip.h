@@ -271,6 +271,23 @@ int trex_tree_gram_skip_x3(const float* S, int N, int64_t K, int skip_rows, floa
                            float* G, void* workspace, int64_t workspace_bytes, void* stream);
 int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64_t K, int row0, int nrows,
                          float max_abs_m, float max_abs_s, float* dS_rows, void* stream);
+/* Leaf-code operand for the MF (Q = 4).  The leaf rows of S are fixed
+ * one-hot data (trex's update_seq keeps sequences[:n_leaves],
+ * tree.py:127-130), so dS = M S can read their codes instead of the f32 rows:
+ * rows [0, lcr), lcr = trex_tree_leaf_code_rows(n_leaf) = 32 floor(n_leaf / 32),
+ * are encoded once by trex_tree_leaf_codes into `codes` ([lcr][L] bytes,
+ * trex_tree_leaf_codes_bytes).  *status (device int) is set to 1 when a row is
+ * not exactly one-hot (the codes must then not be used).
+ * trex_tree_mf_rows_x3_codes returns bitwise the result of trex_tree_mf_rows_x3
+ * (one-hot x scale is exact in f16; the codes expand into the same split
+ * planes) with a quarter of the operand bytes for those rows. */
+int trex_tree_leaf_code_rows(int n_leaf);
+int64_t trex_tree_leaf_codes_bytes(int n_leaf, int L);
+int trex_tree_leaf_codes(const float* S, int n_leaf, int L, int Q, void* codes,
+                         int64_t codes_bytes, int* status, void* stream);
+int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N, int64_t K, int row0,
+                               int nrows, float max_abs_m, float max_abs_s, const void* codes,
+                               int n_leaf, float* dS_rows, void* stream);
 
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */

@@ -410,3 +410,83 @@ def test_gram_is_run_to_run_deterministic(device, N, K, skip, x3):
     for G in runs[1:]:
         assert torch.equal(G[t0:], runs[0][t0:])
     assert torch.equal(runs[0][t0:, t0:], runs[0][t0:, t0:].T)
+
+
+def _onehot_case(N, L, seed, Q=4):
+    rng = np.random.default_rng(seed)
+    nl = (N + 1) // 2
+    x = rng.normal(size=(N, L, Q)) * 3
+    S = np.exp(x - x.max(-1, keepdims=True))
+    S /= S.sum(-1, keepdims=True)
+    S[:nl] = np.eye(Q)[rng.integers(0, Q, size=(nl, L))]
+    return S.reshape(N, L * Q).astype(np.float32), nl
+
+
+@pytest.mark.parametrize("N,L", [(511, 1001), (511, 2048), (255, 333), (383, 64), (127, 50),
+                                 (101, 77)])
+def test_leaf_code_mf_is_bitwise_the_x3_mf(device, N, L):
+    """trex_tree_mf_rows_x3_codes (leaf rows read as codes, one-hot x scale
+    exact in f16) == trex_tree_mf_rows_x3 on the f32 rows bit for bit --
+    ragged last column tile, both column-tile widths, n_leaf not a multiple
+    of 32 (N = 101: 51 leaves, 32 code rows) -- and both vs fp64."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    Sn, nl = _onehot_case(N, L, N + L)
+    K = L * 4
+    S = _t(Sn, device)
+    st = stream_handle(torch.device(device))
+    cb = torch.empty(int(lib().trex_tree_leaf_codes_bytes(nl, L)), dtype=torch.uint8, device=device)
+    status = torch.full((1,), 7, dtype=torch.int32, device=device)
+    check(lib().trex_tree_leaf_codes(ptr(S), nl, L, 4, ptr(cb), cb.numel(), ptr(status), st))
+    Mn = np.random.default_rng(N).normal(size=(N, N)) * 20
+    M = _t(Mn, device)
+    n_anc = N - nl
+    d0 = torch.empty((n_anc, K), device=device)
+    d1 = torch.empty((n_anc, K), device=device)
+    mx = float(np.abs(_n(M)).max())
+    check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, nl, n_anc, mx, 1.0, ptr(d0), st))
+    check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, n_anc, mx, 1.0, ptr(cb), nl,
+                                           ptr(d1), st))
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    assert torch.equal(d0, d1)
+    ref = _n(M)[nl:].astype(np.float64) @ Sn.astype(np.float64)
+    np.testing.assert_allclose(_n(d1), ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+
+
+def test_leaf_codes_flag_rows_that_are_not_one_hot(device):
+    """A leaf row that is not exactly one-hot sets the status word, and the
+    optimiser then keeps the f32-row GEMMs."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    Sn, nl = _onehot_case(127, 40, 3)
+    Sn[5, 7] = 0.5  # site 1 of leaf 5: not one-hot
+    S = _t(Sn, device)
+    cb = torch.empty(int(lib().trex_tree_leaf_codes_bytes(nl, 40)), dtype=torch.uint8, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    check(lib().trex_tree_leaf_codes(ptr(S), nl, 40, 4, ptr(cb), cb.numel(), ptr(status),
+                                     stream_handle(torch.device(device))))
+    torch.cuda.synchronize()
+    assert int(status.item()) == 1
+    params, _, _ = _tree_case(nl, 40, 4, 1)
+    opt = G.TreeOptimizer(S.reshape(127, 40, 4), {k: _t(v, device) for k, v in params.items()},
+                          lr=0.01)
+    assert opt.gemm == "x3" and opt.codes is None
+
+
+def test_tree_optimizer_leaf_codes_are_bitwise_neutral(device, monkeypatch):
+    """TreeOptimizer with leaf codes (the default for one-hot leaves, Q = 4)
+    == TREX_LEAF_CODES=0 (f32 leaf rows) bit for bit, loss and parameters."""
+    params, noise, seqs = _tree_case(100, 50, 4, 9)  # 96 code rows + 4 f32 leaf rows
+    nz = _t(noise, device)
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TREX_LEAF_CODES", flag)
+        opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                              lr=0.01)
+        assert (opt.codes is not None) == (flag == "1")
+        losses = [float(opt.step(max(0.2, 1.5 - 0.2 * i), nz)) for i in range(4)]
+        runs.append((losses, {k: v.clone() for k, v in opt.params.items()}))
+    assert runs[0][0] == runs[1][0]
+    for k in runs[0][1]:
+        assert torch.equal(runs[0][1][k], runs[1][1][k])

@@ -1,0 +1,54 @@
+"""C5 MF with and without leaf codes (trex_tree_leaf_codes): bitwise
+equality of dS, HIP-event times of both paths (and of the Gram)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+if __name__ == "__main__":
+    import torch
+
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    N, L, Q, nl = 511, 50000, 4, 256
+    K = L * Q
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    S = torch.softmax(torch.randn((N, L, Q), device=dev, generator=g) * 3, dim=-1)
+    codes = torch.randint(0, Q, (nl, L), device=dev, generator=g)
+    S[:nl] = torch.nn.functional.one_hot(codes, Q).float()
+    S = S.reshape(N, K).contiguous()
+    M = torch.randn((N, N), device=dev, generator=g) * 50
+    G0 = torch.zeros((N, N), device=dev)
+    d0, d1 = torch.empty((N - nl, K), device=dev), torch.empty((N - nl, K), device=dev)
+    ws = torch.empty(int(lib().trex_tree_workspace_bytes(N, K)), dtype=torch.uint8, device=dev)
+    cb = torch.empty(int(lib().trex_tree_leaf_codes_bytes(nl, L)), dtype=torch.uint8, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = stream_handle(dev)
+    cs = torch.cuda.current_stream(dev)
+    check(lib().trex_tree_leaf_codes(ptr(S), nl, L, Q, ptr(cb), cb.numel(), ptr(status), st))
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0, "leaf rows not one-hot?"
+
+    def timed(fn, reps=20):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cs)
+        for _ in range(reps):
+            fn()
+        e1.record(cs)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    mx = float(N + 1) * 50
+    tg0 = timed(lambda: check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, nl, 1.0, ptr(G0), ptr(ws),
+                                                           ws.numel(), st)))
+    tm0 = timed(lambda: check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, nl, N - nl, mx, 1.0,
+                                                         ptr(d0), st)))
+    tm1 = timed(lambda: check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, N - nl, mx,
+                                                               1.0, ptr(cb), nl, ptr(d1), st)))
+    deq = torch.equal(d0, d1)
+    dd = (d0 - d1).abs().max().item()
+    print(f"gram {tg0:.1f} us  mf {tm0:.1f} us  mf(codes) {tm1:.1f} us  bitwise dS {deq} "
+          f"(max diff {dd:.3g})")

@@ -87,6 +87,12 @@ SIGNATURES = {
     "trex_tree_gram_skip_x3": (_c_i, [_p, _c_i, _c_i64, _c_i, _c_f, _p, _p, _c_i64, _p]),
     "trex_tree_gram_mirror": (_c_i, [_p, _c_i, _c_i, _p]),
     "trex_tree_mf_rows_x3": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p, _p]),
+    # leaf-code MF operand (exact one-hot leaf rows, Q = 4)
+    "trex_tree_leaf_code_rows": (_c_i, [_c_i]),
+    "trex_tree_leaf_codes_bytes": (_c_i64, [_c_i, _c_i]),
+    "trex_tree_leaf_codes": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _c_i64, _p, _p]),
+    "trex_tree_mf_rows_x3_codes": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p, _c_i,
+                                          _p, _p]),
     "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),
     "trex_tree_constraint": (_c_i, [_p, _c_i, _c_f, _c_f, _p, _c_i, _p, _p, _p]),
     "trex_tree_compute_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _p, _p, _p]),

@@ -824,10 +824,16 @@ __device__ __forceinline__ h8 tr_pair(const unsigned char* p, int four_rows) {
 // tile, operands from L2) 386 us; F staged column-major with 64-B row pieces
 // per load + M fragments loaded per lane 320 us; + M staged in full lines
 // 296 us; this 274 us.
-template <int TPC>
+// CODES (Q = 4): the n stages s < lcs (F rows 0 .. 32 lcs: exact one-hot leaf
+// rows) load the rows' codes (codesR [32 lcs][L] bytes, trex_tree_leaf_codes;
+// an F item = one site's 4 states = one byte) instead of F and expand them
+// into the same f16 hi / lo planes (one-hot x sf is exact in f16, lo = 0):
+// bitwise the same result, a quarter of the bytes for those stages
+template <int TPC, bool CODES>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void mf_kernel3(
     const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
-    int nchunks, float* __restrict__ out, float sm, float sf) {
+    int nchunks, float* __restrict__ out, float sm, float sf, const uint8_t* __restrict__ codesR,
+    int lcs) {
   constexpr int CW = TPC * 32;
   constexpr int NIT = 32 * (CW / 4);  // F (row, column group) float4 items per stage
   constexpr int IPT = (NIT + 511) / 512;
@@ -844,6 +850,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int rbase = blockIdx.y * 256 + wave * 32;
   const rsrc_t rm = make_rsrc(Mm, (uint32_t)((size_t)N * N * 4));
   const rsrc_t rf = make_rsrc(F, (uint32_t)((size_t)N * K * 4));
+  // CODES: item (n, cg) reads the code byte of row n, site chunk * CW / 4 + cg
+  // (sites past L read the next row's bytes: columns past K, never stored)
+  const int Lc = K / 4;
+  const rsrc_t rc = make_rsrc(codesR, (uint32_t)(CODES ? (size_t)Lc * 32 * lcs : 0));
+  int cvb[IPT];
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int item = tid + 512 * j;
+    cvb[j] = (item < NIT) ? (item / (CW / 4)) * Lc + item % (CW / 4) : 0x7FFF0000;
+  }
   int fvb[IPT], lofs[IPT];
   bool fok[IPT];
 #pragma unroll
@@ -875,11 +891,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   int fc = blockIdx.x, fs = 0;  // load cursor (chunk, stage)
   int cc = blockIdx.x, cs = 0;  // compute cursor
   auto load = [&](Set& q) {
-    const int so = (fc * CW + fs * 32 * K) * 4;
+    if (CODES && fs < lcs) {
+      const int so = fs * 32 * Lc + fc * (CW / 4);
 #pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-      const int vo = fok[j] ? fvb[j] + so : 0x7FFF0000;
-      q.a[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, vo, 0, 0);
+      for (int j = 0; j < IPT; ++j)
+        q.a[j].x = __builtin_amdgcn_raw_buffer_load_b8(rc, cvb[j] < 0x7FFF0000 ? cvb[j] + so : cvb[j], 0, 0);
+    } else {
+      const int so = (fc * CW + fs * 32 * K) * 4;
+#pragma unroll
+      for (int j = 0; j < IPT; ++j) {
+        const int vo = fok[j] ? fvb[j] + so : 0x7FFF0000;
+        q.a[j] = __builtin_amdgcn_raw_buffer_load_b128(rf, vo, 0, 0);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -888,10 +911,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     q.s = fs;
     if (++fs == nst) { fs = 0; fc += gx; }
   };
+  const uint32_t hb = (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)sf);  // one-hot 1 x sf
   auto stage = [&](unsigned char* buf, const Set& q) {
+    if (CODES && q.s < lcs) {
+#pragma unroll
+      for (int j = 0; j < IPT; ++j) {
+        if (!fok[j]) continue;
+        const uint32_t code = q.a[j].x & 0xFFu;
+        *reinterpret_cast<uint2*>(buf + lofs[j]) =
+            uint2{(code == 0 ? hb : 0u) | ((code == 1 ? hb : 0u) << 16),
+                  (code == 2 ? hb : 0u) | ((code == 3 ? hb : 0u) << 16)};
+        *reinterpret_cast<uint2*>(buf + FPLANE + lofs[j]) = uint2{0u, 0u};
+      }
+    }
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
-      if (!fok[j]) continue;
+      if (!fok[j] || (CODES && q.s < lcs)) continue;
       const uint32_t e[4] = {q.a[j].x, q.a[j].y, q.a[j].z, q.a[j].w};
       h4 hi, lo;
 #pragma unroll
@@ -1507,6 +1542,7 @@ float split_scale(float max_abs) {
 }
 
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
+// x3_max > 0: f16x3 split products with operands bounded by x3_max
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
          hipStream_t st, int t0 = 0, float x3_max = 0.0f) {
   const GramPlan g = gram_plan(N, K, symmetric != 0, t0);
@@ -1804,19 +1840,21 @@ extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t 
   return tree_hip_check("trex_tree_mf_rows");
 }
 
-extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64_t K, int row0,
-                                    int nrows, float max_abs_m, float max_abs_s, float* dS_rows,
-                                    void* stream) {
+namespace {
+// v3 MF launch; codesR / lcs: leaf-code stages (CODES instantiation) or null / 0
+int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int row0, int nrows,
+          float max_abs_m, float max_abs_s, float* dS_rows, const uint8_t* codesR, int lcs,
+          void* stream) {
   if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
       row0 + nrows > N || !pos_finite_f32(max_abs_m) || !pos_finite_f32(max_abs_s))
-    return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3: bad arguments");
+    return set_error(TREX_E_ARG, "%s: bad arguments", fn);
   if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
-    return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows_x3: S exceeds 2 GiB");
+    return set_error(TREX_E_UNSUPPORTED, "%s: S exceeds 2 GiB", fn);
   // float4 operand loads: rows must start 16-B aligned (the last column tile
   // may be ragged: its columns past K are computed from the next row's data
   // and never stored)
   if (K % 4 != 0)
-    return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows_x3: K = L*Q must be a multiple of 4");
+    return set_error(TREX_E_UNSUPPORTED, "%s: K = L*Q must be a multiple of 4", fn);
   // column tiles per workgroup: fewest rounds x tiles over one workgroup per CU
   const int64_t ct = (K + 31) / 32;
   const int rg = (nrows + 255) / 256;
@@ -1836,11 +1874,87 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
     const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
     hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(512), lds, (hipStream_t)stream, M, S, N,
                        (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
-                       split_scale(max_abs_s));
+                       split_scale(max_abs_s), codesR, lcs);
   };
-  if (best == 5) go(mf_kernel3<5>, 5, 2 * (2 * 32 * 320 + 256 * kMfStride));
-  else go(mf_kernel3<4>, 4, 2 * (2 * 32 * 320 + 256 * kMfStride));
-  return tree_hip_check("trex_tree_mf_rows_x3");
+  const int lds = 2 * (2 * 32 * 320 + 256 * kMfStride);
+  const bool codes = codesR && lcs > 0;
+  if (best == 5) {
+    if (codes) go(mf_kernel3<5, true>, 5, lds);
+    else go(mf_kernel3<5, false>, 5, lds);
+  } else {
+    if (codes) go(mf_kernel3<4, true>, 4, lds);
+    else go(mf_kernel3<4, false>, 4, lds);
+  }
+  return tree_hip_check(fn);
+}
+
+// leaf codes of rows [0, lcr): codesR [lcr][L] bytes, the state of each
+// exactly one-hot (row, site); 0xFF and *status = 1 otherwise
+__global__ __launch_bounds__(256) void leaf_codes_kernel(const float* __restrict__ S, int L, int lcr,
+                                                         uint8_t* __restrict__ codesR,
+                                                         int* __restrict__ status) {
+  const int64_t n = (int64_t)lcr * L;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(S)[t];  // row t / L, site t % L, Q = 4
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    int ones = 0, idx = 0;
+    bool clean = true;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (e[q] == 1.0f) {
+        ++ones;
+        idx = q;
+      } else if (e[q] != 0.0f) {
+        clean = false;
+      }
+    }
+    const bool ok = clean && ones == 1;
+    codesR[t] = ok ? (uint8_t)idx : (uint8_t)0xFF;
+    if (!ok) atomicOr(status, 1);
+  }
+}
+}  // namespace
+
+extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64_t K, int row0,
+                                    int nrows, float max_abs_m, float max_abs_s, float* dS_rows,
+                                    void* stream) {
+  return mf_x3("trex_tree_mf_rows_x3", M, S, N, K, row0, nrows, max_abs_m, max_abs_s, dS_rows,
+               nullptr, 0, stream);
+}
+
+extern "C" int trex_tree_leaf_code_rows(int n_leaf) { return n_leaf >= 32 ? 32 * (n_leaf / 32) : 0; }
+
+extern "C" int64_t trex_tree_leaf_codes_bytes(int n_leaf, int L) {
+  const int64_t lcr = trex_tree_leaf_code_rows(n_leaf);
+  return (L <= 0 || lcr <= 0) ? 0 : lcr * L;
+}
+
+extern "C" int trex_tree_leaf_codes(const float* S, int n_leaf, int L, int Q, void* codes,
+                                    int64_t codes_bytes, int* status, void* stream) {
+  const int lcr = trex_tree_leaf_code_rows(n_leaf);
+  if (!S || !codes || !status || L <= 0 || Q != 4 || lcr <= 0 ||
+      (reinterpret_cast<uintptr_t>(S) & 15) != 0)
+    return set_error(TREX_E_ARG, "trex_tree_leaf_codes: bad arguments (Q = 4, n_leaf >= 32, 16-B aligned S)");
+  if (codes_bytes < trex_tree_leaf_codes_bytes(n_leaf, L))
+    return set_error(TREX_E_ARG, "trex_tree_leaf_codes: codes buffer too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(status, 0, sizeof(int), st) != hipSuccess)
+    return set_error(TREX_E_HIP, "trex_tree_leaf_codes: memset failed");
+  const int64_t n = (int64_t)lcr * L;
+  hipLaunchKernelGGL(leaf_codes_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)),
+                     dim3(256), 0, st, S, L, lcr, static_cast<uint8_t*>(codes), status);
+  return tree_hip_check("trex_tree_leaf_codes");
+}
+
+extern "C" int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N, int64_t K,
+                                          int row0, int nrows, float max_abs_m, float max_abs_s,
+                                          const void* codes, int n_leaf, float* dS_rows,
+                                          void* stream) {
+  const int lcr = trex_tree_leaf_code_rows(n_leaf);
+  if (!codes || lcr <= 0 || lcr > N || K % 4 != 0)
+    return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3_codes: bad arguments");
+  return mf_x3("trex_tree_mf_rows_x3_codes", M, S, N, K, row0, nrows, max_abs_m, max_abs_s,
+               dS_rows, static_cast<const uint8_t*>(codes), lcr / 32, stream);
 }
 
 extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,

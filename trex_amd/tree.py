@@ -19,6 +19,8 @@ All arithmetic runs in libtrexhip.so.
 
 from __future__ import annotations
 
+import os
+
 from ._lib import check, lib, ptr, stream_handle
 
 
@@ -374,6 +376,19 @@ class TreeOptimizer:
             self.reducer(self.G)
         self.skip_rows = self.n_leaf
         self.g_row0 = (self.skip_rows // 64) * 64
+        # exact one-hot leaf rows (Q = 4): the x3 MF reads their codes
+        # instead of the f32 rows (bitwise the same dS, trex_tree_leaf_codes);
+        # TREX_LEAF_CODES=0 keeps the f32 rows
+        self.codes = None
+        if (self.gemm == "x3" and self.Q == 4 and lib().trex_tree_leaf_code_rows(self.n_leaf) > 0
+                and os.environ.get("TREX_LEAF_CODES", "1") != "0"):
+            cb = torch.empty(int(lib().trex_tree_leaf_codes_bytes(self.n_leaf, self.L)),
+                             dtype=torch.uint8, device=dev)
+            status = torch.zeros(1, dtype=torch.int32, device=dev)
+            check(lib().trex_tree_leaf_codes(ptr(self.S), self.n_leaf, self.L, self.Q, ptr(cb),
+                                             cb.numel(), ptr(status), stream_handle(dev)))
+            if int(status.item()) == 0:
+                self.codes = cb
 
     def step(self, temperature: float, noise, next_temperature=None):
         """One optimisation step; returns the (device) loss before the update.
@@ -409,7 +424,11 @@ class TreeOptimizer:
         check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
                                       ptr(self.dA), ptr(self.ws), st))
         # d loss / dS for the ancestor rows only (leaf rows are fixed data)
-        if self.gemm == "x3":
+        if self.codes is not None:
+            check(L_.trex_tree_mf_rows_x3_codes(ptr(self.M), ptr(self.S), N, K, self.n_leaf,
+                                                self.n_anc, float(N + 1), 1.0, ptr(self.codes),
+                                                self.n_leaf, ptr(self.dS[self.n_leaf:]), st))
+        elif self.gemm == "x3":
             check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
                                           float(N + 1), 1.0, ptr(self.dS[self.n_leaf:]), st))
         else:
