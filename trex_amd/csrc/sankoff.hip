@@ -1306,15 +1306,6 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
       if (int e = site_run(fn, c, lanes, lp_slots, flag, kg)) return e;
       c.mx_flag = flag;
       c.mx_tiles = site_tiles(L);
-    } else if (mx_eligible(c)) {
-      // the matrix-core kernel first (sankoff_mx.hip); its device flag (a
-      // word in the workspace's tail slack) tells the state-parallel launch
-      // below whether to run
-      int* flag = reinterpret_cast<int*>(static_cast<char*>(workspace) +
-                                         wide_workspace_bytes(B, L, Q) - 128);
-      if (int e = mx_run(fn, c, staged, flag)) return e;
-      c.mx_flag = flag;
-      c.mx_tiles = mx_tiles(L);
     }
     if (use_staged(B, L, Q, s.ni, s.nl, phase)) return staged_run(fn, c, staged);
     return wide_run(fn, c);

@@ -394,7 +394,7 @@ __global__ __launch_bounds__(kReduceThreads) void wide_reduce_kernel(const doubl
   __shared__ double red[kReduceThreads];
   const int b = blockIdx.x;
   if (mx_flag && __hip_atomic_load(mx_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-    // the matrix-core kernel's partials (sankoff_mx.hip): mx_tiles per tree,
+    // the lane-per-site kernel's partials (sankoff_site.hip): mx_tiles per tree,
     // its dC block right after its B * mx_tiles tree partials
     tiles = mx_tiles;
     part_dc = part_tree + (size_t)B * mx_tiles;

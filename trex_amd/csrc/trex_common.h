@@ -96,7 +96,7 @@ struct WideCall {
   float* d_cost;
   void* workspace;
   void* stream;
-  // set when the matrix-core kernel (sankoff_mx.hip) ran first: the device
+  // set when the lane-per-site kernel (sankoff_site.hip) ran first: the device
   // word it wrote (1: it handled the launch -- the state-parallel kernels
   // exit at once, the reduce sums its mx_tiles partials per tree)
   const int* mx_flag = nullptr;
@@ -119,7 +119,7 @@ int staged_run(const char* fn, const WideCall& c, const int32_t* staged);
 // total; tiles is then unused)
 // (first_scale: partials per item, the wide kernel's waves per ragged item)
 // (mx_flag / mx_tiles: when *mx_flag is set on the device, the partials are
-// the matrix-core kernel's, mx_tiles per tree)
+// the lane-per-site kernel's, mx_tiles per tree)
 int partial_reduce(const char* fn, const double* part_tree, const double* part_dc, int B,
                    int tiles, int Q, int phase, float* tree_score, float* d_cost, void* stream,
                    const int* first = nullptr, int first_stride = 0, int items = 0,
@@ -129,11 +129,6 @@ int partial_reduce(const char* fn, const double* part_tree, const double* part_d
 int64_t wide_ragged_workspace_bytes(int64_t items, int Q);
 int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const int* ritem,
                     int64_t items);
-// matrix-core kernel for the factored softmin, 4 < Q <= 20 (sankoff_mx.hip)
-bool mx_eligible(const WideCall& c);
-int mx_tiles(int L);
-size_t mx_lds_bytes(int ni, int nl, int Q);
-int mx_run(const char* fn, const WideCall& c, const int32_t* staged, int* flag);
 // lane-per-site kernel for the factored softmin, 4 < Q <= 20 (sankoff_site.hip)
 bool site_eligible(const WideCall& c, int lp_slots);
 int site_tiles(int L);
