@@ -355,7 +355,7 @@ def c3_line(torch, device, cpu_threads):
            "soft_ms_per_step": soft_s * 1e3, "soft_value": units / soft_s,
            "hard_recon_ms_per_step": hard_s * 1e3, "hard_recon_value": units / hard_s,
            "unit": "site-node-state updates/s",
-           "roofline": {"bound": "hbm", "kernel": "sankoff_wide_kernel<20,soft,fused>+reduce",
+           "roofline": {"bound": "hbm", "kernel": "site_prep + sankoff_site_kernel<3,20> + reduce (lane-per-site, DESIGN 5.8)",
                         "achieved": round(abytes / k_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(abytes / k_s / 1e9 / HBM_PEAK_GBS, 4),
                         "algorithmic_bytes": abytes, "launch_us": round(k_s * 1e6, 2)}}
