@@ -504,7 +504,7 @@ struct KArgs {
 constexpr int kTabFloats = 128;
 constexpr int kWTab = 32;  // (Q + 1) Q <= 20 message floats precede the weights
 #ifndef TREX_ADJ_RING
-#define TREX_ADJ_RING 2
+#define TREX_ADJ_RING 3
 #endif
 #ifndef TREX_ADJ_WPE
 #define TREX_ADJ_WPE 5
