@@ -310,6 +310,12 @@ def test_lane_program_reproduces_oracle(kind):
             return dp[row]
 
         for s in range(S):
+            # the stage's tasks run on different waves at once: the slots it
+            # writes (its rows') and reads (task children's) are disjoint
+            fw = [(int(steps[k][0]) >> 16) & 0xFF for k in range(offs[s], offs[s + 1])]
+            fr = {(int(d) >> 16) & 0xFF for k in range(offs[s], offs[s + 1])
+                  for d in steps[k][1:3] if (int(d) >> 24) & 3 == 2}
+            assert not fr & set(fw) and len(fw) == len(set(fw))
             for k in range(offs[s], offs[s + 1]):
                 w0, da, db, flags = (int(x) for x in steps[k])
                 row, sl = w0 & 0xFFFF, (w0 >> 16) & 0xFF
@@ -337,6 +343,13 @@ def test_lane_program_reproduces_oracle(kind):
         # into its slot at its parent's stage and read at its own stage
         holder = {}
         for s in reversed(range(S)):
+            # a stage's tasks (and, at <= 4 tasks, a task's two children) run
+            # on different waves at once: no slot written in the stage may be
+            # one read in it, and no two writes may share a slot
+            reads = {(int(steps[k][0]) >> 16) & 0xFF for k in range(offs[s], offs[s + 1])}
+            writes = [(int(d) >> 16) & 0xFF for k in range(offs[s], offs[s + 1])
+                      for d in steps[k][1:3] if (int(d) >> 24) & 3 == 2]
+            assert not reads & set(writes) and len(writes) == len(set(writes))
             for k in range(offs[s], offs[s + 1]):
                 w0, da, db, flags = (int(x) for x in steps[k])
                 row, sl = w0 & 0xFFFF, (w0 >> 16) & 0xFF
