@@ -50,6 +50,11 @@ def parse():
     ap.add_argument("--no-ragged", action="store_true", help="skip the ragged-batch line")
     ap.add_argument("--no-shard", action="store_true", help="skip the 128-tree shard line")
     ap.add_argument("--no-e2e", action="store_true", help="skip the H2D-inclusive C4 line")
+    ap.add_argument("--c5-taxa", type=int, default=256, help="C5 leaves (nodes = 2 taxa - 1)")
+    ap.add_argument("--c5-sites", type=int, default=50000,
+                    help="C5 sites (split over the ranks at N > 1)")
+    ap.add_argument("--c5-steps", type=int, default=20)
+    ap.add_argument("--c5-warmup", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/pmc_traffic.py)")
@@ -429,8 +434,8 @@ def c5_gemm_kernels(torch, opt):
                                                        ptr(opt.G), ptr(opt.ws), opt.ws.numel(), st))
         if opt.codes is not None:  # the step's own MF: leaf rows read as codes
             mf = lambda: check(L_.trex_tree_mf_rows_x3_codes(  # noqa: E731
-                ptr(opt.M), ptr(opt.S), N, K, nl, na, float(N + 1), 1.0, ptr(opt.codes), nl,
-                ptr(dS), st))
+                ptr(opt.M), ptr(opt.S), N, K, nl, na, float(N + 1), 1.0, ptr(opt.codes),
+                opt.codes.numel(), nl, opt.Q, ptr(dS), st))
         else:
             mf = lambda: check(L_.trex_tree_mf_rows_x3(ptr(opt.M), ptr(opt.S), N, K, nl, na,  # noqa: E731
                                                        float(N + 1), 1.0, ptr(dS), st))
@@ -476,7 +481,7 @@ def c5_gemm_kernels(torch, opt):
     return out
 
 
-def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3"):
+def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=256, L=50000):
     """C5 (BASELINE.json configs[4]): 256 taxa (511 nodes) x 50 000 sites x 4
     states, joint Adam optimisation step (update_seq, update_tree, surrogate
     + graph constraint, their VJPs, optax Adam) -- trex's
@@ -489,7 +494,7 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3"):
     from trex_amd.distributed import shard_bounds
     from trex_amd.tree import TreeOptimizer, gumbel_noise
 
-    nl, L, Q = 256, 50000, 4
+    Q = 4
     n = 2 * nl - 1
     lo, hi = shard_bounds(L, rank, world)
     seqs = generate_groundtruth(nl, Q, 5, L, seed=6).all_sequences.astype(np.int8)
@@ -535,11 +540,12 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3"):
     step_bytes = n * Kl * 4 + ((n - lcr) * Kl * 4 + lcr * (hi - lo) + na * Kl * 4) + na * Kl * 4 * 8
     gemm_desc = ("f16x3 split-product MFMA GEMMs (f32 accumulate; rtol 1e-5 vs fp64 at this "
                  "size, tests/test_configs_full_gpu.py)" if opt.gemm == "x3" else "f32 MFMA GEMMs")
-    res = {"workload": "C5: 511-node relaxed tree x 50000 sites x 4 states, joint Adam step "
+    res = {"workload": f"C5: {n}-node relaxed tree x {L} sites x {Q} states, joint Adam step "
                        "(surrogate + constraint + VJPs + optax adam), " + gemm_desc
                        + (f"; sites sharded over {world} ranks, Gram all-reduce" if world > 1
                           else ""),
            "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec, "n_gpus": world,
+           "taxa": nl, "sites": L, "sites_rank0": hi - lo if rank == 0 else None,
            "scaling": "strong" if world > 1 else None, "loss_last": float(loss),
            "gemm": opt.gemm, "leaf_codes": opt.codes is not None,
            "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": step_bytes,
@@ -608,8 +614,10 @@ def nk_line(torch, device, steps=50, warmup=5):
                                                device=device)}
         opt = Adam(params, 1e-3)
 
+        gbuf = torch.empty_like(params["ancestors"])
+
         def step():
-            _, g = fn.value_and_grad(params["ancestors"], S0)
+            _, g = fn.value_and_grad(params["ancestors"], S0, out=gbuf)
             opt.step(params, {"ancestors": g})
 
         for _ in range(warmup):
@@ -620,9 +628,24 @@ def nk_line(torch, device, steps=50, warmup=5):
             step()
         torch.cuda.synchronize()
         sec = (time.perf_counter() - t0) / steps
+        # the same step captured once in a hipGraph (the Adam step count lives
+        # on the device, trex_step_advance) and replayed: the reference's
+        # fori_loop body without per-step host launches
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        gsec = (time.perf_counter() - t0) / steps
         out[name] = {"workload": f"{nl} leaves x {L} sites x {Q} states, K={k}, lambda={lam}: "
-                                 "landscape-aware loss + grad + adam step (eager launches)",
-                     "ms_per_step": sec * 1e3,
+                                 "landscape-aware loss + grad + adam step",
+                     "ms_per_step": gsec * 1e3, "ms_per_step_eager": sec * 1e3,
+                     "timing": "hipGraph replay of one captured step (eager launches beside it)",
                      "logit_macs_per_step": 2 * fn.n_parents * L * Q ** (k + 1)}
     return out
 
@@ -825,15 +848,18 @@ def main():
         if not args.no_c3:
             result["c3"] = c3_line(torch, device, threads)
         if not args.no_c5:
-            result["c5"] = c5_line(torch, device)
+            c5kw = dict(steps=args.c5_steps, warmup=args.c5_warmup, nl=args.c5_taxa,
+                        L=args.c5_sites)
+            result["c5"] = c5_line(torch, device, **c5kw)
             torch.cuda.empty_cache()
-            result["c5_f32"] = c5_line(torch, device, gemm="f32")
+            result["c5_f32"] = c5_line(torch, device, gemm="f32", **c5kw)
         if not args.no_nk:
             result["nk"] = nk_line(torch, device)
         if not args.no_ragged:
             result["ragged"] = ragged_line(torch, device)
     if world > 1 and not args.no_c5:
-        result["c5"] = c5_line(torch, device, rank=rank, world=world)
+        result["c5"] = c5_line(torch, device, steps=args.c5_steps, warmup=args.c5_warmup,
+                               rank=rank, world=world, nl=args.c5_taxa, L=args.c5_sites)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

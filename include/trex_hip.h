@@ -48,9 +48,18 @@ extern "C" {
 #define TREX_PLAN_HEADER_INTS 16
 
 const char* trex_last_error(void);
-/* ABI / plan-layout version.  5: plans carry each tree's staged (multi-wave)
- * program after the backtrack entries (trex_plan_ints grew; a binding that
- * sized or cached v4 plans must re-query it), Q up to 64, ragged Q > 4.
+/* ABI / plan-layout version.
+ * 7: graph-capturable optimiser steps (device step state, *_dev entry
+ *    points, trex_gumbel_noise); trex_tree_mf_rows_x3_codes takes the codes
+ *    buffer size and Q.
+ * 6: plans carry each tree's lane programs (the lane-per-site kernel for
+ *    4 < Q <= 20, sankoff_site.hip) after the staged regions -- re-query
+ *    trex_plan_ints; info[0] of trex_plan_build, the n_slots argument of
+ *    trex_sankoff_fwd / _bwd / _fwd_bwd, is a packed word: the LDS stack
+ *    depth | (lane-program slots + 1) << 16 (pass it through unchanged).
+ * 5: plans carry each tree's staged (multi-wave) program after the
+ *    backtrack entries (trex_plan_ints grew; a binding that sized or cached
+ *    v4 plans must re-query it), Q up to 64, ragged Q > 4.
  * 4: site-major DP tables. */
 int trex_version(void);
 
@@ -66,7 +75,10 @@ int trex_version(void);
  * plan [host] int32 buffer of trex_plan_ints(B, n_all) ints; copy it to the
  *   device unchanged before the trex_sankoff_* calls.
  * info [host] int32[4] out: {n_slots, backtrack_ok, n_dag_nodes, n_unreached}
- *   n_slots = LDS stack depth the kernels need (pass to every call);
+ *   n_slots = the packed slot word the kernels need (pass it unchanged to
+ *   every call): bits 0-15 the LDS stack depth of the one-wave kernels,
+ *   bits 16-31 the lane-per-site kernel's slot count + 1 (0: no lane
+ *   programs fit);
  *   backtrack_ok = 0 when the reference's backtrack would not terminate
  *   (cyclic child references, sankoff.py:212-265); pass it on to
  *   trex_sankoff_backtrack, which then refuses with TREX_E_TOPOLOGY.
@@ -287,7 +299,10 @@ int trex_tree_leaf_codes(const float* S, int n_leaf, int L, int Q, void* codes,
                          int64_t codes_bytes, int* status, void* stream);
 int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N, int64_t K, int row0,
                                int nrows, float max_abs_m, float max_abs_s, const void* codes,
-                               int n_leaf, float* dS_rows, void* stream);
+                               int64_t codes_bytes, int n_leaf, int Q, float* dS_rows,
+                               void* stream);
+/* (codes_bytes: the size of `codes`, >= trex_tree_leaf_codes_bytes(n_leaf, K / Q);
+ * Q must be 4 and K = L * Q -- TREX_E_ARG otherwise, never a silent misread.) */
 
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */
@@ -343,6 +358,47 @@ int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, int Q, floa
                               float next_temperature, float* params, float* mu, float* nu,
                               int count, float lr, float b1, float b2, float eps, float* s_next,
                               void* stream);
+
+/* ------------------------------------------------------------------------
+ * Graph-capturable optimisation loops (ABI v7).  The reference runs its
+ * optimiser inside lax.fori_loop / lax.scan (src/trex/evals/benchmark.py:
+ * 167-200; tests/test_convergence.py:238-261 jits the step), i.e. the step
+ * count, the annealed temperature and the Gumbel key are device values.  Here
+ * they live in a device "step state" (trex_step_state_bytes() bytes, zeroed
+ * or holding the count of the steps already taken in its first int32):
+ *   trex_step_advance: count += 1, then Adam's bias corrections
+ *     1 - b^count (b1, b2; computed exactly as the host-count entry points
+ *     do, so both give bitwise the same update) and, when temps [n_temps] is
+ *     given (an annealing schedule on the device), this step's temperature
+ *     T = temps[count - 1] and the next one's Tn = temps[count] (clamped to
+ *     the last entry).  Launch it first in every step.
+ *   *_dev: the entry points above with count / temperature read from the
+ *     state instead of host arguments (trex_tree_constraint_dev: grad_scale =
+ *     T; trex_adam_seq_update_step_dev: temperature = T, next = Tn).
+ *   trex_gumbel_noise: Gumbel(0, 1) noise out f32 [n] for the state's step
+ *     (state NULL: step 0), a pure function of (seed, step, index) -- the
+ *     reference's per-step jax.random.gumbel(step_key) (tree.py:71);
+ *     counter-based splitmix64 draws, restated in oracle/datagen_ref.py.
+ * A step built from these launches only kernels whose arguments do not
+ * change between steps, so it can be captured once in a hipGraph and
+ * replayed (trex_amd.tree.TreeOptimizer.device_loop, trex_amd.tree.Adam). */
+int trex_step_state_bytes(void);
+int trex_step_advance(void* state, float b1, float b2, const float* temps, int64_t n_temps,
+                      void* stream);
+int trex_adam_step_dev(float* params, const float* grads, float* mu, float* nu, int64_t n,
+                       const void* state, float lr, float b1, float b2, float eps,
+                       const double* grad_sq_norm_parts, int n_parts, float clip_norm,
+                       void* stream);
+int trex_optax_step_dev(int kind, float* params, const float* grads, float* state1,
+                        float* state2, int64_t n, const void* state, float lr, float b1, float b2,
+                        float eps, float weight_decay, const double* grad_sq_norm_parts,
+                        int n_parts, float clip_norm, void* stream);
+int trex_adam_seq_update_step_dev(const float* ds_anc, int n_anc, int L, int Q, const void* state,
+                                  float* params, float* mu, float* nu, float lr, float b1,
+                                  float b2, float eps, float* s_next, void* stream);
+int trex_tree_constraint_dev(const float* A, int N, float scale, const void* state, float* loss,
+                             int accumulate, float* dA, void* workspace, void* stream);
+int trex_gumbel_noise(uint64_t seed, const void* state, int64_t n, float* out, void* stream);
 
 /* ========================================================================
  * Ragged batches: trees of different sizes (n_all_b taxa+ancestors) and

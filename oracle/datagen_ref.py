@@ -69,6 +69,18 @@ def uniform_states(seed, n, Q, start=0):
     return (draw(seed, (i >> _U(32)) + _U(1 << 32), i) % _U(Q)).astype(np.int8)
 
 
+def gumbel_noise(seed, step, n):
+    """trex_gumbel_noise (datagen.hip gumbel_kernel): Gumbel(0, 1) noise of
+    device-loop step `step`, f32 [n]; u in (0, 1) from 53 bits + 1/2,
+    -log(-log u) in double."""
+    with np.errstate(over="ignore"):
+        sk = mix64(_U(seed) ^ (_U(0x6A09E667F3BCC909) * _U(step + 1)))
+    i = np.arange(n, dtype=np.uint64)
+    r = draw(sk, _U(0x7FFF0000) + (i >> _U(32)), i)
+    u = ((r >> _U(11)).astype(np.float64) + 0.5) * 2.0 ** -53
+    return (-np.log(-np.log(u))).astype(np.float32)
+
+
 def _unit53(r):
     return float(int(r) >> 11) * 2.0 ** -53
 

@@ -133,6 +133,72 @@ def cond_rtol(dp_ref, tau, rtol=1e-5):
     return max(rtol, 2.0 * 2.0 ** -24 * float(np.abs(dp_ref).max()) / tau)
 
 
+def assert_bound_close(got, ref, bound, what="value"):
+    """Elementwise |got - ref| <= bound (an array of per-entry bounds, e.g.
+    1e-5 * (|M| @ |S|) for a product with mixed signs).  Returns the max of
+    |got - ref| / bound; the message names the worst entry."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    bound = np.broadcast_to(np.asarray(bound, dtype=np.float64), ref.shape)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    err = np.abs(got - ref)
+    ratio = err / np.maximum(bound, 1e-300)
+    k = np.unravel_index(int(np.argmax(np.where(np.isfinite(ratio), ratio, np.inf))), ratio.shape)
+    bad = ~(err <= bound)
+    assert not bad.any(), (f"{what}: max err / bound {ratio[k]:.3e} at {k} (got {got[k]!r}, "
+                           f"ref {ref[k]!r}, bound {bound[k]:.3e}); {int(bad.sum())} of "
+                           f"{bad.size} entries out of bound")
+    return float(ratio[k])
+
+
+def path_dmax(children, dp_ref):
+    """Per (tree, internal row, site): the sum over the row and its ancestors
+    (root included) of max_state |D|.  children (B, n_all, 2) trex child ids;
+    dp_ref (B, n_int, Q, L) the oracle's table.  A marginal is a product of
+    softmin weights along the path from the root, each weight's exponent
+    (D_j - min D) / tau carrying fp32 D's rounding, ~eps |D| / tau, so the
+    relative error of a marginal entry is bounded by ~eps * path_dmax / tau
+    (shared children of trex's DAG quirk: the larger path)."""
+    B, n_int, _, L = dp_ref.shape
+    n_all = children.shape[1]
+    nl = n_all - n_int
+    dm = np.abs(dp_ref).max(axis=2)  # (B, n_int, L)
+    out = np.zeros_like(dm)
+    for b in range(B):
+        parents = [[] for _ in range(n_int)]
+        for node in range(nl, n_all):
+            for c in children[b, node]:
+                c = int(c)
+                if nl <= c < node:
+                    parents[c - nl].append(node - nl)
+        for r in range(n_int - 1, -1, -1):
+            up = 0.0
+            for p in parents[r]:
+                up = np.maximum(up, out[b, p])
+            out[b, r] = dm[b, r] + up
+    return out
+
+
+def marginal_rtol(children, dp_ref, tau, rtol=1e-5, c=4.0):
+    """Per-entry relative bound for softmin marginals vs the fp64 oracle,
+    (B, n_int, 1, L): max(rtol, c * 2^-24 * path_dmax / tau) -- fp32 D's
+    conditioning along the root path (see path_dmax), never below 1e-5."""
+    return np.maximum(rtol, c * 2.0 ** -24 * path_dmax(children, dp_ref) / tau)[:, :, None, :]
+
+
+def assert_marginals_close(got, ref, children, dp_ref, tau, c=4.0, what="marginals"):
+    """Elementwise marginal bar: |got - ref| <= marginal_rtol * |ref| + 1e-30
+    (1e-30: entries fp32 cannot hold near its underflow).  Returns the max
+    relative error over entries with |ref| > 1e-30 and the bound used."""
+    rt = marginal_rtol(children, dp_ref, tau, c=c)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert_bound_close(got, ref, rt * np.abs(ref) + 1e-30, what=what)
+    m = np.abs(ref) > 1e-30
+    rel = np.abs(np.asarray(got, np.float64) - ref)[m] / np.abs(ref)[m]
+    return float(rel.max()) if rel.size else 0.0, rt
+
+
 __all__ = ["simulate_leaves", "hamming", "int_cost", "random_leaves", "balanced_children",
            "weird_children", "random_topologies", "create_balanced_binary_tree",
-           "assert_grad_close", "cond_rtol"]
+           "assert_grad_close", "cond_rtol", "assert_bound_close", "path_dmax", "marginal_rtol",
+           "assert_marginals_close"]

@@ -56,3 +56,20 @@ def test_temperatures_reject_bad_values(bad):
     L = lib()
     assert L.trex_tree_update_tree(p, None, None, 7, 3, bad, p, None) == TREX_E_ARG
     assert L.trex_tree_update_tree_bwd(p, p, None, 7, 3, bad, p, None) == TREX_E_ARG
+
+
+@pytest.mark.parametrize("Q,short", [(5, False), (2, False), (4, True)])
+def test_leaf_code_mf_rejects_wrong_alphabet_or_short_buffer(Q, short):
+    """trex_tree_mf_rows_x3_codes reads one code byte per (code row, site) of
+    a Q = 4 alphabet: any other Q, or a codes buffer smaller than
+    trex_tree_leaf_codes_bytes(n_leaf, K / Q), is TREX_E_ARG."""
+    b = _buf()
+    p = b.ctypes.data
+    L = lib()
+    N, n_leaf, sites = 127, 64, 100
+    K = sites * Q
+    need = int(L.trex_tree_leaf_codes_bytes(n_leaf, sites))
+    rc = L.trex_tree_mf_rows_x3_codes(p, p, N, K, n_leaf, N - n_leaf, 128.0, 1.0, p,
+                                      need - 1 if short else need, n_leaf, Q, p, None)
+    assert rc == TREX_E_ARG, rc
+    assert b"codes" in L.trex_last_error()

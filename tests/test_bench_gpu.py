@@ -76,3 +76,37 @@ def test_bench_world2_device_share_sums_the_whole_batch(tmp_path):
     # fp32 rounding of the sum
     assert_grad_close(red[:q2].reshape(states, states), dc.cpu().numpy(), rtol=1e-6)
     np.testing.assert_allclose(red[q2], float(f.tree_score.double().sum()), rtol=1e-6)
+
+
+def test_bench_world2_c5_site_shard_matches_single_process():
+    """The bench's N > 1 C5 leg (site shard, Gram all-reduce of the ancestor
+    rows + mirror, MAX-reduced timer) at a small shape: 128 taxa (255 nodes,
+    cached leaf block rows [0, 128)), 510 sites -> 255 per rank, K = 1 020
+    (K % 16 = 12, a ragged last x3 chunk).  Rank 0 prints a c5 line with
+    n_gpus == 2, and its loss after the run equals bench's own single-process
+    C5 leg over all sites (same seeds, same schedule) at rtol 1e-5."""
+    taxa, sites, steps, warmup = 128, 510, 4, 2
+    env = dict(os.environ, TREX_BENCH_DEVICE_SHARE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--trees", "16", "--taxa", "16",
+           "--sites", "256", "--c5-taxa", str(taxa), "--c5-sites", str(sites),
+           "--c5-steps", str(steps), "--c5-warmup", str(warmup)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    c5 = json.loads(lines[0])["c5"]
+    assert c5["n_gpus"] == 2 and c5["scaling"] == "strong"
+    assert c5["taxa"] == taxa and c5["sites"] == sites and c5["sites_rank0"] == sites // 2
+    assert c5["gemm"] == "x3"
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    single = bench.c5_line(torch, torch.device("cuda", 0), steps=steps, warmup=warmup, nl=taxa,
+                           L=sites)
+    assert single["n_gpus"] == 1
+    np.testing.assert_allclose(c5["loss_last"], single["loss_last"], rtol=1e-5)

@@ -103,12 +103,12 @@ def _c5_case(nl=32, L=512, Q=4, seed=3):
     return S, params, noise
 
 
-def _c5_worker(rank, world, port, clip, L, out):
+def _c5_worker(rank, world, port, clip, L, nl, out):
     dev = _init(rank, world, port)
     from trex_amd.distributed import shard_bounds
     from trex_amd.tree import TreeOptimizer
 
-    S, params, noise = _c5_case(L=L)
+    S, params, noise = _c5_case(nl=nl, L=L)
     L = S.shape[1]
     lo, hi = shard_bounds(L, rank, world)
     t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
@@ -121,31 +121,45 @@ def _c5_worker(rank, world, port, clip, L, out):
     assert single.gemm == "x3" and shard.gemm == "x3", (single.gemm, shard.gemm)
     temps = [2.0, 1.5, 1.2, 1.0]
     l1, l2 = [], []
+    gerr = 0.0
     for i, T_ in enumerate(temps):
         nxt = temps[i + 1] if i + 1 < len(temps) else T_
         l1.append(float(single.step(T_, nz, next_temperature=nxt)))
         l2.append(float(shard.step(T_, nz, next_temperature=nxt)))
+        if i == 0:
+            # same parameters before the first step: the sharded Gram (cached
+            # leaf x leaf block, reduced ancestor rows, mirrored leaf rows'
+            # ancestor columns) == the single-process Gram elementwise
+            g1 = single.G.cpu().numpy().astype(np.float64)
+            g2 = shard.G.cpu().numpy().astype(np.float64)
+            gerr = float((np.abs(g2 - g1) / np.maximum(np.abs(g1), 1e-30)).max())
     torch.cuda.synchronize()
+    assert shard.g_row0 == (nl // 64) * 64
     out[rank] = (np.array(l1), np.array(l2),
                  single.params["tree_params"].cpu().numpy(),
                  shard.params["tree_params"].cpu().numpy(),
                  single.params["ancestors"][:, lo:hi].cpu().numpy(),
-                 shard.params["ancestors"].cpu().numpy())
+                 shard.params["ancestors"].cpu().numpy(), gerr)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("clip,L", [(None, 512), (1.0, 512), (None, 510)])
-def test_c5_site_sharding_world2_on_one_gpu(clip, L):
+@pytest.mark.parametrize("clip,L,nl", [(None, 512, 32), (1.0, 512, 32), (None, 510, 32),
+                                       (None, 510, 100), (1.0, 256, 100)])
+def test_c5_site_sharding_world2_on_one_gpu(clip, L, nl):
     """L = 510: each rank holds 255 sites, K = 1 020 (K % 16 = 12, like the
     C5 shard at N = 8, K = 25 000): the x3 GEMMs run on the ragged K and the
     cached leaf x leaf Gram survives sharding (only the ancestor rows are
-    all-reduced per step, then mirrored)."""
+    all-reduced per step, then mirrored).  nl = 100 (N = 199): the cached
+    leaf block ends at row 64 < n_leaf, so the per-step reduce covers rows
+    [64, 199) and the mirror rewrites the leaf rows' ancestor columns; the
+    first step's Gram is checked elementwise against the single process."""
     world = 2
     out = mp.Manager().dict()
-    mp.spawn(_c5_worker, args=(world, _free_port(), clip, L, out), nprocs=world, join=True)
+    mp.spawn(_c5_worker, args=(world, _free_port(), clip, L, nl, out), nprocs=world, join=True)
     for r in range(world):
-        l1, l2, tp1, tp2, an1, an2 = out[r]
+        l1, l2, tp1, tp2, an1, an2, gerr = out[r]
+        assert gerr <= 1e-5, gerr
         np.testing.assert_allclose(l2, l1, rtol=1e-5)
         # Gram partial sums differ in association from the single-process
         # Gram only at fp32 rounding; Adam's ~sign(g) first steps can turn a

@@ -154,3 +154,47 @@ def test_run_landscape_aware_adam_matches_oracle_loop(device):
     top2 = np.sort(p, axis=-1)[..., -2:]  # skip near-ties in the argmax
     clear = (top2[..., 1] - top2[..., 0]) > 1e-3
     np.testing.assert_array_equal(out.cpu().numpy()[clear], p.argmax(-1)[clear])
+
+
+def test_nk_adam_step_graph_replay_is_bitwise_eager(device):
+    """The reference's eval shape (32 leaves, 15 sites, Q = 2, K = 10;
+    benchmark.py:981-985): one landscape-aware loss + grad + Adam step
+    captured in a hipGraph (the Adam count lives on the device,
+    trex_step_advance) and replayed 6 times == 6 eager steps, bitwise; and the
+    device-count Adam == the host-count trex_adam_step, bitwise."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+    from trex_amd.tree import Adam
+
+    c = _case(32, 15, 2, 10, seed=5)
+    land = NK.NKLandscape(c["inter"], c["F"], 2, device)
+    S0 = torch.as_tensor(c["S0"], device=device)
+    runs = []
+    for mode in ("eager", "graph", "host"):
+        fn = NK.LandscapeAwareLoss(c["A"], c["n_leaves"], land, 3.0, 10)
+        params = {"ancestors": torch.as_tensor(c["anc"], device=device).clone()}
+        opt = Adam(params, 1e-3)
+        g = torch.empty_like(params["ancestors"])
+        mu, nu = torch.zeros_like(g), torch.zeros_like(g)
+
+        def step(k):
+            fn.value_and_grad(params["ancestors"], S0, out=g)
+            if mode == "host":  # the pre-v7 host-count update
+                check(lib().trex_adam_step(ptr(params["ancestors"]), ptr(g), ptr(mu), ptr(nu),
+                                           g.numel(), k, 1e-3, 0.9, 0.999, 1e-8, None, 0, 0.0,
+                                           stream_handle(device)))
+            else:
+                opt.step(params, {"ancestors": g})
+
+        if mode == "graph":
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step(0)
+            for _ in range(6):
+                graph.replay()
+        else:
+            for k in range(1, 7):
+                step(k)
+        torch.cuda.synchronize()
+        runs.append((float(fn.loss[0]), params["ancestors"].clone()))
+    assert runs[1][0] == runs[0][0] and torch.equal(runs[1][1], runs[0][1])
+    assert runs[2][0] == runs[0][0] and torch.equal(runs[2][1], runs[0][1])

@@ -226,11 +226,12 @@ def test_adjacency_roundtrip():
 
 
 def test_abi_version_matches_plan_layout():
-    """trex_version() 6: plans carry the lane-per-site program of every tree
-    after the staged programs, and info[0] packs its slot count above the
-    stack depth (include/trex_hip.h); a binding that sized v5 plans itself
-    must see the bump."""
-    assert lib().trex_version() == 6
+    """trex_version() >= 6: plans carry the lane-per-site program of every
+    tree after the staged programs, and info[0] packs its slot count above
+    the stack depth (include/trex_hip.h); a binding that sized v5 plans
+    itself must see the bump.  7 added the device step state (no plan
+    change)."""
+    assert lib().trex_version() == 7
     ch = balanced_children(64, B=1)
     p = TreePlan(ch)
     assert p.n_slots == 5 and p.lane_slots == 12 and p.slot_word == 5 | (13 << 16)

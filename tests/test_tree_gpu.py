@@ -293,6 +293,24 @@ def test_mf_rows_equals_full_dS_slice(device, N, K, row0):
     np.testing.assert_allclose(_n(full), ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("N,row0", [(199, 64), (511, 256), (130, 128), (64, 0), (64, 64)])
+def test_gram_mirror_restores_symmetry(device, N, row0):
+    """trex_tree_gram_mirror: after a site-sharded all-reduce of rows
+    [row0, N) only, G[i][j] = G[j][i] for i < row0 <= j; the leaf x leaf
+    block [0, row0)^2 and rows [row0, N) are untouched.  Starting from a full
+    symmetric Gram whose upper-right block is garbage, the result equals the
+    full Gram bitwise."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    rng = np.random.default_rng(N + row0)
+    S = rng.random((N, 40))
+    full = _t(S @ S.T, device)
+    G = full.clone()
+    G[:row0, row0:] = -3.0
+    check(lib().trex_tree_gram_mirror(ptr(G), N, row0, stream_handle(torch.device(device))))
+    assert torch.equal(G, full)
+
+
 def test_gram_skip_keeps_cached_block(device):
     """trex_tree_gram_skip recomputes every tile except the leading constant
     block, which keeps its previous contents (the optimiser's cached
@@ -445,8 +463,8 @@ def test_leaf_code_mf_is_bitwise_the_x3_mf(device, N, L):
     d1 = torch.empty((n_anc, K), device=device)
     mx = float(np.abs(_n(M)).max())
     check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, nl, n_anc, mx, 1.0, ptr(d0), st))
-    check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, n_anc, mx, 1.0, ptr(cb), nl,
-                                           ptr(d1), st))
+    check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, n_anc, mx, 1.0, ptr(cb),
+                                           cb.numel(), nl, 4, ptr(d1), st))
     torch.cuda.synchronize()
     assert int(status.item()) == 0
     assert torch.equal(d0, d1)
@@ -490,3 +508,38 @@ def test_tree_optimizer_leaf_codes_are_bitwise_neutral(device, monkeypatch):
     assert runs[0][0] == runs[1][0]
     for k in runs[0][1]:
         assert torch.equal(runs[0][1][k], runs[1][1][k])
+
+
+@pytest.mark.parametrize("gemm,capture", [("x3", True), ("f32", True), ("x3", False)])
+def test_tree_device_loop_is_bitwise_eager(device, gemm, capture):
+    """TreeOptimizer.device_loop (count, annealed temperature and Gumbel noise
+    on the device; one step captured in a hipGraph and replayed) == eager
+    step(T_k, gumbel_noise_step(seed, k), T_{k+1}) for k = 1..5, bitwise:
+    losses, tree params and ancestor logits -- including after 2 eager steps
+    (the device count continues the host one)."""
+    params, _, seqs = _tree_case(16, 52, 4, 19)
+    temps = [max(0.1, 2.0 * (1.0 - k / 50)) for k in range(12)]
+    seed = 1234
+    ref = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                          lr=0.01, gemm=gemm)
+    dut = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                          lr=0.01, gemm=gemm)
+    shape = (ref.N - 1, ref.n_anc)
+    for k in range(1, 3):  # both start with two eager steps
+        for o in (ref, dut):
+            o.step(temps[k - 1], G.gumbel_noise_step(seed, k, shape, device), temps[k])
+    loop = dut.device_loop(temps, seed, capture=capture)
+    losses = []
+    for k in range(3, 8):
+        losses.append(float(ref.step(temps[k - 1], G.gumbel_noise_step(seed, k, shape, device),
+                                     temps[k])))
+        assert float(loop.run(1)) == losses[-1], k
+    torch.cuda.synchronize()
+    assert dut.opt.count == ref.opt.count == 7
+    for k in ref.params:
+        assert torch.equal(dut.params[k], ref.params[k]), k
+    # the device noise is trex_gumbel_noise's restatement (oracle/datagen_ref.py)
+    from oracle.datagen_ref import gumbel_noise
+
+    np.testing.assert_allclose(_n(G.gumbel_noise_step(seed, 3, shape, device)).ravel(),
+                               gumbel_noise(seed, 3, shape[0] * shape[1]), rtol=1e-6, atol=1e-7)

@@ -47,7 +47,8 @@ if __name__ == "__main__":
     tm0 = timed(lambda: check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, nl, N - nl, mx, 1.0,
                                                          ptr(d0), st)))
     tm1 = timed(lambda: check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, N - nl, mx,
-                                                               1.0, ptr(cb), nl, ptr(d1), st)))
+                                                               1.0, ptr(cb), cb.numel(), nl, 4,
+                                                               ptr(d1), st)))
     deq = torch.equal(d0, d1)
     dd = (d0 - d1).abs().max().item()
     print(f"gram {tg0:.1f} us  mf {tm0:.1f} us  mf(codes) {tm1:.1f} us  bitwise dS {deq} "

@@ -91,8 +91,8 @@ SIGNATURES = {
     "trex_tree_leaf_code_rows": (_c_i, [_c_i]),
     "trex_tree_leaf_codes_bytes": (_c_i64, [_c_i, _c_i]),
     "trex_tree_leaf_codes": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _c_i64, _p, _p]),
-    "trex_tree_mf_rows_x3_codes": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p, _c_i,
-                                          _p, _p]),
+    "trex_tree_mf_rows_x3_codes": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p,
+                                          _c_i64, _c_i, _c_i, _p, _p]),
     "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),
     "trex_tree_constraint": (_c_i, [_p, _c_i, _c_f, _c_f, _p, _c_i, _p, _p, _p]),
     "trex_tree_compute_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _p, _p, _p]),
@@ -105,6 +105,17 @@ SIGNATURES = {
                                          _c_f, _c_f, _c_f, _p, _p]),
     "trex_adam_seq_step": (_c_i, [_p, _p, _c_i, _c_i, _c_i, _c_f, _p, _p, _p, _c_i, _c_f, _c_f,
                                   _c_f, _c_f, _p, _p]),
+    # device step state: graph-capturable optimisation loops (ABI v7)
+    "trex_step_state_bytes": (_c_i, []),
+    "trex_step_advance": (_c_i, [_p, _c_f, _c_f, _p, _c_i64, _p]),
+    "trex_adam_step_dev": (_c_i, [_p, _p, _p, _p, _c_i64, _p, _c_f, _c_f, _c_f, _c_f, _p, _c_i,
+                                  _c_f, _p]),
+    "trex_optax_step_dev": (_c_i, [_c_i, _p, _p, _p, _p, _c_i64, _p, _c_f, _c_f, _c_f, _c_f,
+                                   _c_f, _p, _c_i, _c_f, _p]),
+    "trex_adam_seq_update_step_dev": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _p, _p, _p, _c_f, _c_f,
+                                             _c_f, _c_f, _p, _p]),
+    "trex_tree_constraint_dev": (_c_i, [_p, _c_i, _c_f, _p, _p, _c_i, _p, _p, _p]),
+    "trex_gumbel_noise": (_c_i, [ctypes.c_uint64, _p, _c_i64, _p, _p]),
     # synthetic data on the device
     "trex_datagen_workspace_bytes": (_c_i64, [_c_i, _c_i]),
     "trex_datagen_groundtruth": (_c_i, [ctypes.c_uint64, _c_i, _c_i, _c_i, _c_i, _p, _p, _c_i64,

@@ -96,6 +96,23 @@ __global__ __launch_bounds__(256) void uniform_states_kernel(uint64_t seed, int6
 // (counters 4b .. 4b + 2), stream 4n + 2: new states (counter b L + i),
 // stream 4n + 3: independent-mutation mask.
 __device__ __forceinline__ double unit53(uint64_t r) { return (double)(r >> 11) * 0x1.0p-53; }
+
+// Gumbel(0, 1) noise for step `count` of a device loop -- the reference's
+// fresh jax.random.gumbel(step_key) per step (tree.py:71,
+// tests/test_convergence.py:258-261) as a pure function of (seed, step,
+// index): u = (r >> 11 + 1/2) 2^-53 in (0, 1), g = -log(-log u) in double,
+// rounded to f32 (restated in oracle/datagen_ref.py).  count: the device
+// step state's first word (trex_step_advance), NULL = step 0.
+__global__ __launch_bounds__(256) void gumbel_kernel(uint64_t seed, const int* __restrict__ count,
+                                                     int64_t n, float* __restrict__ out) {
+  const uint64_t step = count ? (uint64_t)(uint32_t)count[0] : 0ull;
+  const uint64_t sk = mix64(seed ^ (0x6A09E667F3BCC909ull * (step + 1ull)));
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint64_t r = draw(sk, 0x7FFF0000ull + (uint64_t)(i >> 32), (uint64_t)i);
+    const double u = ((double)(r >> 11) + 0.5) * 0x1.0p-53;
+    out[i] = (float)(-log(-log(u)));
+  }
+}
 __device__ __forceinline__ float unit24(uint64_t r) { return (float)(r >> 40) * 0x1.0p-24f; }
 
 __device__ __forceinline__ int64_t nk_fixed(float v) { return (int64_t)((double)v * 0x1.0p40); }
@@ -221,6 +238,17 @@ extern "C" int trex_datagen_groundtruth(uint64_t seed, int n_leaves, int L, int 
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return TREX_OK;
+}
+
+extern "C" int trex_gumbel_noise(uint64_t seed, const void* state, int64_t n, float* out,
+                                 void* stream) {
+  if (n <= 0 || !out) return set_error(TREX_E_ARG, "trex_gumbel_noise: bad arguments");
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(gumbel_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     (hipStream_t)stream, seed, static_cast<const int*>(state), n, out);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "trex_gumbel_noise: %s", hipGetErrorString(e));
   return TREX_OK;
 }
 

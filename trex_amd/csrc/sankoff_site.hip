@@ -630,7 +630,26 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     // leaf / 1e5 children of a row with cotangent g
     auto leafish_adj = [&](const float (&g)[kSQ], int d0, int d1) {
       const int k0 = (d0 >> 24) & 3, k1 = (d1 >> 24) & 3;
-      if (k0 == kKindLeaf || k1 == kKindLeaf) leaf_hist(g, d0, d1);
+      if (k0 == kKindLeaf || k1 == kKindLeaf) {
+        leaf_hist(g, d0, d1);
+        // a missing / out-of-range leaf state (code Q: trex's dropped scatter
+        // leaves the all-1e5 row, sankoff.py:152) sends the T[Q] message,
+        // which depends on C through log sum_j K_ij: its adjoint is the 1e5
+        // row's (r_i = g_i / sum_j K_ij, u = 1), per lane, times the number
+        // of such leaf children.  The histogram's column Q is discarded.
+        const int nmiss = (k0 == kKindLeaf && leaf_code(d0) == Q ? 1 : 0) +
+                          (k1 == kKindLeaf && leaf_code(d1) == Q ? 1 : 0);
+        if (__any(active && nmiss != 0)) {
+          const float fm = active ? (float)nmiss : 0.0f;
+          float r[kSQ], u[kSQ];
+#pragma unroll
+          for (int i = 0; i < kSQ; ++i) {
+            r[i] = fm * (g[i] * sinv[i]);
+            u[i] = i < Q ? 1.0f : 0.0f;
+          }
+          outer(r, u);
+        }
+      }
       if (k0 == 0) sent_adj(g);
       if (k1 == 0) sent_adj(g);
     };

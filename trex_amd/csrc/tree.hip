@@ -663,10 +663,53 @@ __global__ __launch_bounds__(256) void gram_mirror_kernel(float* __restrict__ G,
   }
 }
 
+// Device step state of a graph-capturable optimisation loop
+// (trex_step_advance): the 1-based step count and what the step's kernels
+// derive from it -- Adam's bias corrections and the annealing schedule's
+// temperature of this step and the next -- so a captured step replays with
+// the right values (the reference's lax.fori_loop / scan carry,
+// src/trex/evals/benchmark.py:167-200).  A null state pointer: host values.
+struct StepState {
+  int count;
+  float bc1, bc2, T, Tn;
+  float pad[3];
+};
+static_assert(sizeof(StepState) == 32, "step state layout");
+
+// b^n by squaring in IEEE double: the host entry points and
+// trex_step_advance compute the same bits (no pow() implementations to
+// disagree, no contraction under -ffp-contract=off)
+__host__ __device__ inline double ipow_d(double b, int n) {
+  double r = 1.0;
+  while (n > 0) {
+    if (n & 1) r = r * b;
+    b = b * b;
+    n >>= 1;
+  }
+  return r;
+}
+__host__ __device__ inline float bias_corr(float b, int count) {
+  return (float)(1.0 - ipow_d((double)b, count));
+}
+
+__global__ void step_advance_kernel(StepState* __restrict__ st, float b1, float b2,
+                                    const float* __restrict__ temps, int64_t n_temps) {
+  const int k = st->count + 1;
+  st->count = k;
+  st->bc1 = bias_corr(b1, k);
+  st->bc2 = bias_corr(b2, k);
+  if (temps && n_temps > 0) {
+    st->T = temps[(int64_t)k - 1 < n_temps ? k - 1 : n_temps - 1];
+    st->Tn = temps[(int64_t)k < n_temps ? k : n_temps - 1];
+  }
+}
+
 __global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict__ v, int n,
                                                       float scale, float* __restrict__ out,
-                                                      int accumulate) {
+                                                      int accumulate,
+                                                      const StepState* __restrict__ ss = nullptr) {
   __shared__ double sh[256];
+  if (ss) scale = ss->T;
   double s = 0.0;
   for (int t = threadIdx.x; t < n; t += 256) s += v[t];
   s = block_sum_256(s, sh);
@@ -1072,8 +1115,10 @@ __global__ __launch_bounds__(256) void soft_combine_kernel(const float* __restri
 __global__ __launch_bounds__(256) void constraint_kernel(const float* __restrict__ A, int N,
                                                         float scale, float gscale,
                                                         double* __restrict__ colloss,
-                                                        float* __restrict__ dA) {
+                                                        float* __restrict__ dA,
+                                                        const StepState* __restrict__ ss) {
   __shared__ double sh[256];
+  if (ss) gscale = ss->T;
   const int n_anc = (N - 1) / 2;
   const int c = N - n_anc + blockIdx.x;
   double s = 0.0;
@@ -1157,7 +1202,12 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
                                                   int64_t n, float lr, float b1, float b2,
                                                   float eps, float bc1, float bc2,
                                                   const double* __restrict__ sqnorm,
-                                                  int nparts, float clip) {
+                                                  int nparts, float clip,
+                                                  const StepState* __restrict__ ss) {
+  if (ss) {
+    bc1 = ss->bc1;
+    bc2 = ss->bc2;
+  }
   float scale = 1.0f;
   if (sqnorm) {
     double s = 0.0;
@@ -1193,7 +1243,12 @@ __global__ __launch_bounds__(256) void optax_kernel(int kind, float* __restrict_
                                                    float b1, float b2, float eps, float wd,
                                                    float bc1, float bc2,
                                                    const double* __restrict__ sqnorm,
-                                                   int nparts, float clip) {
+                                                   int nparts, float clip,
+                                                   const StepState* __restrict__ ss) {
+  if (ss) {
+    bc1 = ss->bc1;
+    bc2 = ss->bc2;
+  }
   float scale = 1.0f;
   if (sqnorm) {
     double sum = 0.0;
@@ -1318,8 +1373,14 @@ template <int QT>
 __global__ __launch_bounds__(256) void adam_seq_update_kernel(
     const float* __restrict__ ds, int64_t rows, int Qr, float T, float Tn, float* __restrict__ p,
     float* __restrict__ mu, float* __restrict__ nu, float lr, float b1, float b2, float eps,
-    float bc1, float bc2, float* __restrict__ s_out) {
+    float bc1, float bc2, float* __restrict__ s_out, const StepState* __restrict__ ss) {
   const int Q = QT ? QT : Qr;
+  if (ss) {
+    bc1 = ss->bc1;
+    bc2 = ss->bc2;
+    T = ss->T;
+    Tn = ss->Tn;
+  }
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
     float pv[QT ? QT : 32], mv[QT ? QT : 32], vv[QT ? QT : 32], gv[QT ? QT : 32],
         sv[QT ? QT : 32];
@@ -1601,7 +1662,8 @@ extern "C" int trex_tree_surrogate(const float* S, const float* A, int N, int64_
   if (int e = gram(S, S, N, K, 1, G, part, st)) return e;
   hipLaunchKernelGGL(surrogate_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, dA,
                      dS ? M : nullptr, rowloss);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0,
+                     (const StepState*)nullptr);
   if (dS) {
     const int nrowt = (N + 63) / 64;
     const int ncolb = (int)((K + 63) / 64);
@@ -1642,7 +1704,8 @@ extern "C" int trex_tree_soft_cost(const float* S, const float* A, const float* 
   // G[i][j] = <S_i, W_j> (not symmetric for a general C): all tile pairs
   if (int e = gram(S, Wp, N, K, ckind == 0 ? 1 : 0, G, part, st)) return e;
   hipLaunchKernelGGL(soft_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, rowloss);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0,
+                     (const StepState*)nullptr);
   return tree_hip_check("trex_tree_soft_cost");
 }
 
@@ -1655,10 +1718,26 @@ extern "C" int trex_tree_constraint(const float* A, int N, float scale, float gr
   hipStream_t st = (hipStream_t)stream;
   double* colloss = static_cast<double*>(workspace);
   hipLaunchKernelGGL(constraint_kernel, dim3(n_anc), dim3(256), 0, st, A, N, scale, grad_scale,
-                     colloss, dA);
+                     colloss, dA, (const StepState*)nullptr);
   hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, colloss, n_anc, grad_scale,
-                     loss, accumulate);
+                     loss, accumulate, (const StepState*)nullptr);
   return tree_hip_check("trex_tree_constraint");
+}
+
+extern "C" int trex_tree_constraint_dev(const float* A, int N, float scale, const void* state,
+                                        float* loss, int accumulate, float* dA, void* workspace,
+                                        void* stream) {
+  if (!A || !loss || !workspace || !state || N < 3)
+    return set_error(TREX_E_ARG, "trex_tree_constraint_dev: bad arguments");
+  const int n_anc = (N - 1) / 2;
+  hipStream_t st = (hipStream_t)stream;
+  double* colloss = static_cast<double*>(workspace);
+  const StepState* ss = static_cast<const StepState*>(state);
+  hipLaunchKernelGGL(constraint_kernel, dim3(n_anc), dim3(256), 0, st, A, N, scale, 0.0f, colloss,
+                     dA, ss);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, colloss, n_anc, 0.0f, loss,
+                     accumulate, ss);
+  return tree_hip_check("trex_tree_constraint_dev");
 }
 
 extern "C" int trex_tree_compute_cost(const float* S, const float* A, const float* subst, int N,
@@ -1670,7 +1749,8 @@ extern "C" int trex_tree_compute_cost(const float* S, const float* A, const floa
   // rows 0..N-2 only ([:-1] in tree.py:296)
   hipLaunchKernelGGL(compute_cost_kernel, dim3(N - 1), dim3(256), 0, st, S, A, subst, N, L, Q,
                      rowcost);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowcost, N - 1, 1.0f, cost, 0);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowcost, N - 1, 1.0f, cost, 0,
+                     (const StepState*)nullptr);
   return tree_hip_check("trex_tree_compute_cost");
 }
 
@@ -1680,12 +1760,35 @@ extern "C" int trex_adam_step(float* params, const float* grads, float* mu, floa
                               void* stream) {
   if (!params || !grads || !mu || !nu || n < 0 || count < 1)
     return set_error(TREX_E_ARG, "trex_adam_step: bad arguments");
-  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
-  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  const float bc1 = bias_corr(b1, count);
+  const float bc2 = bias_corr(b2, count);
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, params,
                      grads, mu, nu, n, lr, b1, b2, eps, bc1, bc2, grad_sq_norm_parts, n_parts,
-                     clip_norm);
+                     clip_norm, (const StepState*)nullptr);
   return tree_hip_check("trex_adam_step");
+}
+
+extern "C" int trex_step_state_bytes(void) { return (int)sizeof(StepState); }
+
+extern "C" int trex_step_advance(void* state, float b1, float b2, const float* temps,
+                                 int64_t n_temps, void* stream) {
+  if (!state || (temps && n_temps <= 0))
+    return set_error(TREX_E_ARG, "trex_step_advance: bad arguments");
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream,
+                     static_cast<StepState*>(state), b1, b2, temps, n_temps);
+  return tree_hip_check("trex_step_advance");
+}
+
+extern "C" int trex_adam_step_dev(float* params, const float* grads, float* mu, float* nu,
+                                  int64_t n, const void* state, float lr, float b1, float b2,
+                                  float eps, const double* grad_sq_norm_parts, int n_parts,
+                                  float clip_norm, void* stream) {
+  if (!params || !grads || !mu || !nu || n < 0 || !state)
+    return set_error(TREX_E_ARG, "trex_adam_step_dev: bad arguments");
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, params,
+                     grads, mu, nu, n, lr, b1, b2, eps, 1.0f, 1.0f, grad_sq_norm_parts, n_parts,
+                     clip_norm, static_cast<const StepState*>(state));
+  return tree_hip_check("trex_adam_step_dev");
 }
 
 extern "C" int trex_optax_step(int kind, float* params, const float* grads, float* state1,
@@ -1695,12 +1798,26 @@ extern "C" int trex_optax_step(int kind, float* params, const float* grads, floa
   if (kind < 0 || kind > 3 || !params || !grads || n < 0 || count < 1 ||
       ((kind != 3) && !state1) || ((kind != 2) && !state2))
     return set_error(TREX_E_ARG, "trex_optax_step: bad arguments");
-  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
-  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  const float bc1 = bias_corr(b1, count);
+  const float bc2 = bias_corr(b2, count);
   hipLaunchKernelGGL(optax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, kind,
                      params, grads, state1, state2, n, lr, b1, b2, eps, weight_decay, bc1, bc2,
-                     grad_sq_norm_parts, n_parts, clip_norm);
+                     grad_sq_norm_parts, n_parts, clip_norm, (const StepState*)nullptr);
   return tree_hip_check("trex_optax_step");
+}
+
+extern "C" int trex_optax_step_dev(int kind, float* params, const float* grads, float* state1,
+                                   float* state2, int64_t n, const void* state, float lr, float b1,
+                                   float b2, float eps, float weight_decay,
+                                   const double* grad_sq_norm_parts, int n_parts, float clip_norm,
+                                   void* stream) {
+  if (kind < 0 || kind > 3 || !params || !grads || n < 0 || !state ||
+      ((kind != 3) && !state1) || ((kind != 2) && !state2))
+    return set_error(TREX_E_ARG, "trex_optax_step_dev: bad arguments");
+  hipLaunchKernelGGL(optax_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, kind,
+                     params, grads, state1, state2, n, lr, b1, b2, eps, weight_decay, 1.0f, 1.0f,
+                     grad_sq_norm_parts, n_parts, clip_norm, static_cast<const StepState*>(state));
+  return tree_hip_check("trex_optax_step_dev");
 }
 
 extern "C" int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n_anc, int L,
@@ -1710,8 +1827,8 @@ extern "C" int trex_adam_seq_step(const float* s_anc, const float* ds_anc, int n
   if (!s_anc || !ds_anc || !params || !mu || !nu || n_anc <= 0 || L <= 0 || Q < 2 || Q > 32 ||
       count < 1 || !pos_finite_f32(temperature))
     return set_error(TREX_E_ARG, "trex_adam_seq_step: bad arguments");
-  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
-  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  const float bc1 = bias_corr(b1, count);
+  const float bc2 = bias_corr(b2, count);
   const int64_t rows = (int64_t)n_anc * L;
   const bool al = ((reinterpret_cast<uintptr_t>(s_anc) | reinterpret_cast<uintptr_t>(ds_anc) |
                     reinterpret_cast<uintptr_t>(params) | reinterpret_cast<uintptr_t>(mu) |
@@ -1735,8 +1852,8 @@ extern "C" int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, 
   if (!ds_anc || !params || !mu || !nu || !s_next || n_anc <= 0 || L <= 0 || Q < 2 || Q > 32 ||
       count < 1 || !pos_finite_f32(temperature) || !pos_finite_f32(next_temperature))
     return set_error(TREX_E_ARG, "trex_adam_seq_update_step: bad arguments");
-  const float bc1 = (float)(1.0 - std::pow((double)b1, (double)count));
-  const float bc2 = (float)(1.0 - std::pow((double)b2, (double)count));
+  const float bc1 = bias_corr(b1, count);
+  const float bc2 = bias_corr(b2, count);
   const int64_t rows = (int64_t)n_anc * L;
   const bool al = ((reinterpret_cast<uintptr_t>(ds_anc) | reinterpret_cast<uintptr_t>(params) |
                     reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
@@ -1745,12 +1862,34 @@ extern "C" int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, 
   if (Q == 4 && al)
     hipLaunchKernelGGL(adam_seq_update_kernel<4>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
                        rows, Q, temperature, next_temperature, params, mu, nu, lr, b1, b2, eps,
-                       bc1, bc2, s_next);
+                       bc1, bc2, s_next, (const StepState*)nullptr);
   else
     hipLaunchKernelGGL(adam_seq_update_kernel<0>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
                        rows, Q, temperature, next_temperature, params, mu, nu, lr, b1, b2, eps,
-                       bc1, bc2, s_next);
+                       bc1, bc2, s_next, (const StepState*)nullptr);
   return tree_hip_check("trex_adam_seq_update_step");
+}
+
+extern "C" int trex_adam_seq_update_step_dev(const float* ds_anc, int n_anc, int L, int Q,
+                                             const void* state, float* params, float* mu,
+                                             float* nu, float lr, float b1, float b2, float eps,
+                                             float* s_next, void* stream) {
+  if (!ds_anc || !params || !mu || !nu || !s_next || !state || n_anc <= 0 || L <= 0 || Q < 2 ||
+      Q > 32)
+    return set_error(TREX_E_ARG, "trex_adam_seq_update_step_dev: bad arguments");
+  const int64_t rows = (int64_t)n_anc * L;
+  const bool al = ((reinterpret_cast<uintptr_t>(ds_anc) | reinterpret_cast<uintptr_t>(params) |
+                    reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
+                    reinterpret_cast<uintptr_t>(s_next)) & 15) == 0;
+  hipStream_t st = (hipStream_t)stream;
+  const StepState* ss = static_cast<const StepState*>(state);
+  if (Q == 4 && al)
+    hipLaunchKernelGGL(adam_seq_update_kernel<4>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
+                       rows, Q, 1.0f, 1.0f, params, mu, nu, lr, b1, b2, eps, 1.0f, 1.0f, s_next, ss);
+  else
+    hipLaunchKernelGGL(adam_seq_update_kernel<0>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
+                       rows, Q, 1.0f, 1.0f, params, mu, nu, lr, b1, b2, eps, 1.0f, 1.0f, s_next, ss);
+  return tree_hip_check("trex_adam_seq_update_step_dev");
 }
 
 extern "C" int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts,
@@ -1821,7 +1960,8 @@ extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N
   double* rowloss = static_cast<double*>(workspace);
   hipLaunchKernelGGL(surrogate_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, dA, M,
                      rowloss);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rowloss, N, 1.0f, loss, 0,
+                     (const StepState*)nullptr);
   return tree_hip_check("trex_tree_surrogate_combine");
 }
 
@@ -1948,11 +2088,15 @@ extern "C" int trex_tree_leaf_codes(const float* S, int n_leaf, int L, int Q, vo
 
 extern "C" int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N, int64_t K,
                                           int row0, int nrows, float max_abs_m, float max_abs_s,
-                                          const void* codes, int n_leaf, float* dS_rows,
-                                          void* stream) {
+                                          const void* codes, int64_t codes_bytes, int n_leaf,
+                                          int Q, float* dS_rows, void* stream) {
   const int lcr = trex_tree_leaf_code_rows(n_leaf);
-  if (!codes || lcr <= 0 || lcr > N || K % 4 != 0)
-    return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3_codes: bad arguments");
+  if (!codes || lcr <= 0 || lcr > N || Q != 4 || K % 4 != 0)
+    return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3_codes: bad arguments (Q = 4 codes only)");
+  // one code byte per (code row, site): the buffer trex_tree_leaf_codes filled
+  if (codes_bytes < (int64_t)lcr * (K / Q))
+    return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3_codes: codes buffer smaller than "
+                                 "trex_tree_leaf_codes_bytes(n_leaf, K / Q)");
   return mf_x3("trex_tree_mf_rows_x3_codes", M, S, N, K, row0, nrows, max_abs_m, max_abs_s,
                dS_rows, static_cast<const uint8_t*>(codes), lcr / 32, stream);
 }

@@ -50,10 +50,15 @@ class Optimizer:
         self.count = 0
         dev = next(iter(params.values())).device
         self.parts = torch.zeros(512 * max(1, len(params)), dtype=torch.float64, device=dev)
+        # device step count + bias corrections (graph-capturable steps)
+        from .tree import step_state
+
+        self.state = step_state(dev)
 
     def step(self, params: dict, grads: dict):
         self.count += 1
         st = stream_handle(next(iter(params.values())).device)
+        check(lib().trex_step_advance(ptr(self.state), self.b1, self.b2, None, 0, st))
         keys = sorted(params)
         nparts = 0
         if self.clip is not None:
@@ -62,9 +67,9 @@ class Optimizer:
                                                ptr(self.parts[512 * i:]), 512, st))
             nparts = 512 * len(keys)
         for k in keys:
-            check(lib().trex_optax_step(
+            check(lib().trex_optax_step_dev(
                 self.kind, ptr(params[k]), ptr(grads[k]), ptr(self.s1[k]), ptr(self.s2[k]),
-                params[k].numel(), self.count, self.lr, self.b1, self.b2, self.eps, self.wd,
+                params[k].numel(), ptr(self.state), self.lr, self.b1, self.b2, self.eps, self.wd,
                 ptr(self.parts) if nparts else None, nparts, float(self.clip or 0.0), st))
 
 

@@ -152,8 +152,10 @@ class LandscapeAwareLoss:
         nb = int(L_.trex_nk_workspace_bytes(self.N, self.L, self.Q, k, self.n_parents))
         self.nk_ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)
 
-    def value_and_grad(self, ancestors, masked_sequences, *, want_grad: bool = True):
-        """(loss (1,) device tensor, d loss / d ancestors (n_anc, L, Q))."""
+    def value_and_grad(self, ancestors, masked_sequences, *, want_grad: bool = True, out=None):
+        """(loss (1,) device tensor, d loss / d ancestors (n_anc, L, Q)).
+        ``out``: a preallocated (n_anc, L, Q) gradient buffer (no allocation:
+        the call launches only kernels and is hipGraph-capturable)."""
         torch = _torch()
         L_ = lib()
         dev = self.S.device
@@ -183,7 +185,7 @@ class LandscapeAwareLoss:
             dS = self.dS_sur
         if not want_grad:
             return self.loss, None
-        d_anc = torch.empty_like(anc)
+        d_anc = torch.empty_like(anc) if out is None else out
         check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaves:]), ptr(dS[self.n_leaves:]),
                                           n_anc, self.L, self.Q, self.T, ptr(d_anc), st))
         return self.loss, d_anc

@@ -60,6 +60,30 @@ def gumbel_noise(shape, generator=None, device=None):
     return -torch.log(-torch.log(u.clamp_min(1e-20)))
 
 
+def step_state(device, count: int = 0):
+    """A device step state (trex_step_advance, include/trex_hip.h) holding
+    `count` steps already taken."""
+    torch = _torch()
+    nwords = int(lib().trex_step_state_bytes()) // 4
+    st = torch.zeros(nwords, dtype=torch.int32, device=device)
+    if count:
+        st[0] = int(count)
+    return st
+
+
+def gumbel_noise_step(seed: int, step: int, shape, device=None, out=None):
+    """The Gumbel noise a device loop draws at (1-based) step `step`
+    (trex_gumbel_noise: a pure function of seed, step and index)."""
+    torch = _torch()
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=device)
+    st = step_state(device, step)
+    check(lib().trex_gumbel_noise(int(seed) & (2**64 - 1), ptr(st), out.numel(), ptr(out),
+                                  stream_handle(device)))
+    return out
+
+
 # ---------------------------------------------------------------------------
 # topology / sequences
 # ---------------------------------------------------------------------------
@@ -266,10 +290,18 @@ class Adam:
         self.count = 0
         dev = next(iter(params.values())).device
         self.parts = torch.zeros(512 * max(1, len(params)), dtype=torch.float64, device=dev)
+        # the step count and bias corrections live on the device (advanced by
+        # a kernel each step), so a step captured in a hipGraph replays with
+        # the right count (trex_step_advance; bitwise the host-count update)
+        self.state = step_state(dev)
 
     def step(self, params: dict, grads: dict):
+        """One update; launches only kernels (graph-capturable unless the
+        clip norm is all-reduced over a process group)."""
         self.count += 1
         st = stream_handle(next(iter(params.values())).device)
+        check(lib().trex_step_advance(ptr(self.state), float(self.b1), float(self.b2), None, 0,
+                                      st))
         keys = sorted(params)
         nparts = 0
         if self.clip is not None:
@@ -286,11 +318,11 @@ class Adam:
             p, g = params[k], grads[k]
             if not (p.is_contiguous() and g.is_contiguous()):
                 raise ValueError("params and grads must be contiguous")
-            check(lib().trex_adam_step(ptr(p), ptr(g), ptr(self.mu[k]), ptr(self.nu[k]),
-                                       p.numel(), self.count, float(self.lr), float(self.b1),
-                                       float(self.b2), float(self.eps),
-                                       ptr(self.parts) if nparts else None, nparts,
-                                       float(self.clip or 0.0), st))
+            check(lib().trex_adam_step_dev(ptr(p), ptr(g), ptr(self.mu[k]), ptr(self.nu[k]),
+                                           p.numel(), ptr(self.state), float(self.lr),
+                                           float(self.b1), float(self.b2), float(self.eps),
+                                           ptr(self.parts) if nparts else None, nparts,
+                                           float(self.clip or 0.0), st))
 
 
 class TreeOptimizer:
@@ -427,7 +459,8 @@ class TreeOptimizer:
         if self.codes is not None:
             check(L_.trex_tree_mf_rows_x3_codes(ptr(self.M), ptr(self.S), N, K, self.n_leaf,
                                                 self.n_anc, float(N + 1), 1.0, ptr(self.codes),
-                                                self.n_leaf, ptr(self.dS[self.n_leaf:]), st))
+                                                self.codes.numel(), self.n_leaf, self.Q,
+                                                ptr(self.dS[self.n_leaf:]), st))
         elif self.gemm == "x3":
             check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
                                           float(N + 1), 1.0, ptr(self.dS[self.n_leaf:]), st))
@@ -442,6 +475,9 @@ class TreeOptimizer:
             # update_seq_bwd + Adam.step
             o = self.opt
             o.count += 1
+            # keep the device step state in step with the host count (a
+            # later device_loop continues from it)
+            check(L_.trex_step_advance(ptr(o.state), float(o.b1), float(o.b2), None, 0, st))
             check(L_.trex_adam_step(ptr(p["tree_params"]), ptr(self.grads["tree_params"]),
                                     ptr(o.mu["tree_params"]), ptr(o.nu["tree_params"]),
                                     p["tree_params"].numel(), o.count, float(o.lr), float(o.b1),
@@ -461,3 +497,110 @@ class TreeOptimizer:
                                               self.Q, T, ptr(self.grads["ancestors"]), st))
             self.opt.step(self.params, self.grads)
         return self.loss
+
+    # ------------------------------------------------------------------
+    # device loop (graph-capturable step)
+    # ------------------------------------------------------------------
+    def device_loop(self, temperatures, noise_seed: int, *, capture: bool = True):
+        """The optimisation loop with everything per-step on the device --
+        the reference's jitted train_step loop (tests/test_convergence.py:
+        238-261; lax.fori_loop in src/trex/evals/benchmark.py:167-200):
+        step k (1-based, continuing this optimiser's count) anneals at
+        temperatures[k - 1] (the next step's temperature is temperatures[k],
+        for update_seq folded into the Adam pass) and draws its Gumbel noise
+        from trex_gumbel_noise(noise_seed, k).  With ``capture`` one step is
+        captured in a hipGraph and replayed; otherwise the same launches run
+        eagerly.  Bitwise the same as ``step(temperatures[k - 1],
+        gumbel_noise_step(noise_seed, k, ...), temperatures[k])``.  Needs
+        no clipping and no process group (the sharded Gram all-reduce is a
+        host collective)."""
+        return _TreeDeviceLoop(self, temperatures, noise_seed, capture)
+
+
+class _TreeDeviceLoop:
+    def __init__(self, opt: TreeOptimizer, temperatures, noise_seed: int, capture: bool):
+        torch = _torch()
+        if opt.opt.clip is not None or opt.group is not None:
+            raise ValueError("device_loop: clip_norm / site sharding are host-driven; use step()")
+        self.opt = opt
+        dev = opt.S.device
+        self.temps = torch.as_tensor(temperatures, dtype=torch.float32).to(dev).contiguous()
+        self.n_temps = self.temps.numel()
+        self.host_temps = [float(t) for t in self.temps.cpu()]
+        self.seed = int(noise_seed) & (2**64 - 1)
+        self.noise = torch.empty((opt.N - 1, opt.n_anc), dtype=torch.float32, device=dev)
+        self.graph = None
+        k0 = opt.opt.count  # steps taken so far
+        if k0 >= self.n_temps:
+            raise ValueError("temperatures must cover the next step")
+        T0 = self.host_temps[k0]
+        if opt._s_temperature != T0:  # S rows at the first step's temperature
+            check(lib().trex_tree_update_seq(ptr(opt.params["ancestors"]), opt.n_anc, opt.L,
+                                             opt.Q, T0, ptr(opt.S[opt.n_leaf:]),
+                                             stream_handle(dev)))
+            opt._s_temperature = T0
+        if capture:
+            # capture records launches without running them: the state
+            # advances only on replays
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._launch()
+
+    def _launch(self):
+        o = self.opt
+        L_ = lib()
+        st = stream_handle(o.S.device)
+        p = o.params
+        N, K = o.N, o.K
+        a = o.opt
+        state = ptr(a.state)
+        check(L_.trex_step_advance(state, float(a.b1), float(a.b2), ptr(self.temps), self.n_temps,
+                                   st))
+        check(L_.trex_gumbel_noise(self.seed, state, self.noise.numel(), ptr(self.noise), st))
+        check(L_.trex_tree_update_tree(ptr(p["tree_params"]), ptr(self.noise), None, N, o.n_anc,
+                                       1.0, ptr(o.A), st))
+        if o.gemm == "x3":
+            check(L_.trex_tree_gram_skip_x3(ptr(o.S), N, K, o.skip_rows, 1.0, ptr(o.G),
+                                            ptr(o.ws), o.ws.numel(), st))
+        else:
+            check(L_.trex_tree_gram_skip(ptr(o.S), N, K, o.skip_rows, ptr(o.G), ptr(o.ws),
+                                         o.ws.numel(), st))
+        check(L_.trex_tree_surrogate_combine(ptr(o.A), ptr(o.G), N, ptr(o.loss), ptr(o.dA),
+                                             ptr(o.M), ptr(o.ws), st))
+        check(L_.trex_tree_constraint_dev(ptr(o.A), N, o.scale, state, ptr(o.loss), 1, ptr(o.dA),
+                                          ptr(o.ws), st))
+        dS = o.dS[o.n_leaf:]
+        if o.codes is not None:
+            check(L_.trex_tree_mf_rows_x3_codes(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc,
+                                                float(N + 1), 1.0, ptr(o.codes), o.codes.numel(),
+                                                o.n_leaf, o.Q, ptr(dS), st))
+        elif o.gemm == "x3":
+            check(L_.trex_tree_mf_rows_x3(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc,
+                                          float(N + 1), 1.0, ptr(dS), st))
+        else:
+            check(L_.trex_tree_mf_rows(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc, ptr(dS), st))
+        check(L_.trex_tree_update_tree_bwd(ptr(o.A), ptr(o.dA), None, N, o.n_anc, 1.0,
+                                           ptr(o.grads["tree_params"]), st))
+        check(L_.trex_adam_step_dev(ptr(p["tree_params"]), ptr(o.grads["tree_params"]),
+                                    ptr(a.mu["tree_params"]), ptr(a.nu["tree_params"]),
+                                    p["tree_params"].numel(), state, float(a.lr), float(a.b1),
+                                    float(a.b2), float(a.eps), None, 0, 0.0, st))
+        check(L_.trex_adam_seq_update_step_dev(ptr(dS), o.n_anc, o.L, o.Q, state,
+                                               ptr(p["ancestors"]), ptr(a.mu["ancestors"]),
+                                               ptr(a.nu["ancestors"]), float(a.lr), float(a.b1),
+                                               float(a.b2), float(a.eps), ptr(o.S[o.n_leaf:]), st))
+
+    def run(self, n_steps: int):
+        """n_steps steps (graph replays or eager launches); returns the
+        (device) loss of the last one."""
+        o = self.opt
+        if o.opt.count + n_steps > self.n_temps:
+            raise ValueError("the temperature schedule does not cover these steps")
+        for _ in range(int(n_steps)):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._launch()
+            o.opt.count += 1
+        o._s_temperature = self.host_temps[min(o.opt.count, self.n_temps - 1)]
+        return o.loss
