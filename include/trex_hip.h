@@ -107,8 +107,10 @@ int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
  *            rows; a lane's Q states are one 8/12/16-byte access for Q <= 4,
  *            a lane group's row for the lane-per-state kernels, Q > 4)
  *   site_score fp32 [B][L] or NULL;  tree_score fp32 [B] (required)
- * Q up to 64 (codon alphabets; leaf codes and ancestral states are int8);
- * Q > 64 returns TREX_E_UNSUPPORTED.
+ * Q up to 128 (leaf codes and ancestral states are int8): Q <= 64 on the
+ * state-parallel / lane-per-site kernels, 64 < Q <= 128 on the large-alphabet
+ * kernel (sankoff_bigq.hip, since ABI v7); Q > 128 returns
+ * TREX_E_UNSUPPORTED.  Ragged batches stop at Q = 64.
  * ---------------------------------------------------------------------- */
 int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
                      const float* cost, int B, int L, int n_all, int Q, float tau,

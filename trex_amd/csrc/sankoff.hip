@@ -1094,9 +1094,9 @@ struct Shape {
 int check_shape(const char* fn, int B, int L, int n_all, int Q, Shape* sh) {
   if (B <= 0 || L <= 0 || n_all < 3 || n_all > 65535 || Q < 2)
     return set_error(TREX_E_ARG, "%s: bad shape B=%d L=%d n_all=%d Q=%d", fn, B, L, n_all, Q);
-  if (Q > kWideMaxQ)
-    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build", fn, Q,
-                     kWideMaxQ);
+  if (Q > kBigMaxQ)
+    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build (int8 leaf "
+                     "codes / ancestral states)", fn, Q, kBigMaxQ);
   sh->B = B;
   sh->L = L;
   sh->n_all = n_all;
@@ -1294,6 +1294,7 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
     c.d_cost = d_cost;
     c.workspace = workspace;
     c.stream = stream;
+    if (Q > kWideMaxQ) return bigq_run(fn, c);  // 64 < Q <= 128 (sankoff_bigq.hip)
     const int32_t* staged = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 6;
     const int32_t* lanes = staged + (int64_t)B * staged_tree_ints(s.ni);
     if (site_eligible(c, lp_slots)) {
@@ -1384,6 +1385,7 @@ extern "C" int trex_dp_site_major(int Q) {
 
 extern "C" int64_t trex_workspace_bytes(int B, int L, int n_all, int Q) {
   if (B <= 0 || L <= 0 || Q <= 0) return 0;
+  if (Q > kWideMaxQ) return bigq_workspace_bytes(B, L, Q);
   if (Q > 4) return wide_workspace_bytes(B, L, Q);
   const int64_t nb = (int64_t)B * tiles_for(L, 1);
   const int64_t narrow = counters_bytes(B) + nb * 8 * (1 + (int64_t)Q * Q) + (int64_t)Q * Q * B * 8 + 256;
@@ -1444,6 +1446,7 @@ extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, con
   if (!plan || !cost || !dp || !anc_states)
     return set_error(TREX_E_ARG, "trex_sankoff_backtrack: null pointer argument");
   const int32_t* bt32 = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 4;
+  if (Q > kWideMaxQ) return bigq_backtrack(bt32, cost, dp, B, L, s.ni, Q, anc_states, stream);
   // every uniform batch: the split-lane kernels of sankoff_wide.hip (4 lanes
   // per site for Q <= 4, 8 for Q <= 32, one lane per site for codons); the
   // sites-per-lane sankoff_backtrack_kernel serves ragged Q <= 4 batches
@@ -1452,7 +1455,7 @@ extern "C" int trex_sankoff_backtrack(const int32_t* plan, int backtrack_ok, con
 
 extern "C" int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int B, int L,
                                       int n_all, int Q, float* out, void* stream) {
-  if (B <= 0 || L <= 0 || n_all < 3 || Q < 2 || Q > kWideMaxQ || !dp || !leaves || !out)
+  if (B <= 0 || L <= 0 || n_all < 3 || Q < 2 || Q > kBigMaxQ || !dp || !leaves || !out)
     return set_error(TREX_E_ARG, "trex_dp_to_trex_layout: bad arguments");
   const int nl = (n_all + 1) / 2;
   const size_t total = (size_t)B * n_all * L;

@@ -308,7 +308,11 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     const cptr<float> KT = K + kSQ * kSQ;
 #pragma unroll 2
     for (int j = 0; j < Q; ++j) {
+#ifdef SITE_DIAG_NOSMEM  // diagnostic: one K column for every j (loads hoisted; wrong math)
+      const cptr<float> kc = KT;
+#else
       const cptr<float> kc = KT + j * kSQ;
+#endif
       const float uj = xu[j * kWave + lane];
 #pragma unroll
       for (int i = 0; i < kSQ; i += 2) s2[i / 2] = __builtin_elementwise_fma(pk(kc[i], kc[i + 1]), pk(uj, uj), s2[i / 2]);
@@ -488,6 +492,10 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     // acc1 += r u^T over the wave's 64 sites (MFMA k = 2 sites)
     // acc1 += (scratch r)(scratch u)^T, the scratch already written
     auto outer_mfma = [&]() {
+#ifdef SITE_DIAG_NOMFMA  // diagnostic: no dC outer products (wrong dC)
+      wave_sync();
+      return;
+#endif
 #pragma unroll
       for (int t4 = 0; t4 < 8; ++t4) {
         const int sg = khalf * 32 + 4 * t4;
@@ -516,6 +524,9 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     // sites per v_mfma_f32_32x32x16_bf16 (12 per 64 sites instead of 32
     // 32x32x2 f32 MFMAs)
     auto leaf_hist = [&](const float (&g)[kSQ], int d0, int d1) {
+#ifdef SITE_DIAG_NOMFMA
+      return;
+#endif
 #pragma unroll
       for (int i = 0; i < kSQ; ++i) xr[swz(i, lane)] = g[i];
       wave_sync();
@@ -587,7 +598,11 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
       for (int j = 0; j < kSQ / 2; ++j) t2[j] = pk(0.0f, 0.0f);
 #pragma unroll 2
       for (int i = 0; i < Q; ++i) {
+#ifdef SITE_DIAG_NOSMEM
+        const cptr<float> kr = K;
+#else
         const cptr<float> kr = K + i * kSQ;
+#endif
         const float ri = xr[swz(i, lane)];
 #pragma unroll
         for (int j = 0; j < kSQ; j += 2)

@@ -103,6 +103,14 @@ struct WideCall {
   int mx_tiles = 0;
 };
 constexpr int kWideMaxQ = 64;
+// 64 < Q <= 128: the large-alphabet kernel (sankoff_bigq.hip; int8 leaf codes
+// and ancestral states bound Q by 128)
+constexpr int kBigMaxQ = 128;
+int bigq_tiles(int L);
+int64_t bigq_workspace_bytes(int B, int L, int Q);
+int bigq_run(const char* fn, const WideCall& c);
+int bigq_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
+                   int Q, int8_t* anc, void* stream);
 constexpr int kRaggedMeta = 12;  // ints per tree record of a ragged plan (plan.cpp)  // leaf codes and ancestral states are int8
 int wide_group(int Q);
 int wide_tiles(int L, int Q);
