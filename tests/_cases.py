@@ -179,14 +179,19 @@ def path_dmax(children, dp_ref):
     return out
 
 
-def marginal_rtol(children, dp_ref, tau, rtol=1e-5, c=4.0):
+def marginal_rtol(children, dp_ref, tau, rtol=1e-5, c=8.0):
     """Per-entry relative bound for softmin marginals vs the fp64 oracle,
     (B, n_int, 1, L): max(rtol, c * 2^-24 * path_dmax / tau) -- fp32 D's
-    conditioning along the root path (see path_dmax), never below 1e-5."""
+    conditioning along the root path (see path_dmax), never below 1e-5.
+    c = 8: measured on MI355X over every kernel and the tests' shapes (Q 4 ..
+    61, tau 0.02 .. 1, 8 .. 64 taxa, C3 at full size), the worst entry sat at
+    5.0 x eps * path_dmax / tau (tools/parity_probe.py marg,
+    profiles/r04_parity_probe.log); entries whose bound is 1e-5 stayed below
+    3e-6."""
     return np.maximum(rtol, c * 2.0 ** -24 * path_dmax(children, dp_ref) / tau)[:, :, None, :]
 
 
-def assert_marginals_close(got, ref, children, dp_ref, tau, c=4.0, what="marginals"):
+def assert_marginals_close(got, ref, children, dp_ref, tau, c=8.0, what="marginals"):
     """Elementwise marginal bar: |got - ref| <= marginal_rtol * |ref| + 1e-30
     (1e-30: entries fp32 cannot hold near its underflow).  Returns the max
     relative error over entries with |ref| > 1e-30 and the bound used."""
@@ -198,7 +203,37 @@ def assert_marginals_close(got, ref, children, dp_ref, tau, c=4.0, what="margina
     return float(rel.max()) if rel.size else 0.0, rt
 
 
+def clear_argmax_mask(ref, rt, slack=4.0):
+    """Sites / rows where the fp64 marginals' top two states differ by more
+    than `slack` times their per-entry bounds: the soft ancestral state there
+    is the fp64 argmax (elsewhere a tie within fp32 conditioning).
+    ref (B, n_int, Q, L), rt (B, n_int, 1, L)."""
+    top2 = np.sort(ref, axis=2)[:, :, -2:, :]
+    return (top2[:, :, 1] - top2[:, :, 0]) > slack * rt[:, :, 0] * top2[:, :, 1] + 1e-30
+
+
+def surrogate_grad_bounds(S, A, rtol=1e-5, constraint_grad=None):
+    """Per-entry bounds for the surrogate's gradients (tree.py:163-209), fp64:
+    dS = (r + c) S - (A + A^T) S  ->  rtol (|r + c| |S| + |A + A^T| |S|);
+    dA = (E_i + E_j) / 2 - G_ij (+ T * constraint)  ->  rtol ((E_i + E_j) / 2
+    + |G_ij| + |constraint term|): the sum of the magnitudes of each entry's
+    terms, the rounding bound of any fp32 evaluation (entries that cancel to
+    ~0 keep an absolute bound from their terms)."""
+    S = np.asarray(S, dtype=np.float64)
+    A = np.asarray(A, dtype=np.float64)
+    F = S.reshape(S.shape[0], -1)
+    G = F @ F.T
+    E = np.diag(G)
+    rc = A.sum(axis=1) + A.sum(axis=0)
+    AA = np.abs(A + A.T)
+    bS = rtol * (np.abs(rc)[:, None] * np.abs(F) + AA @ np.abs(F))
+    bA = 0.5 * (E[:, None] + E[None, :]) + np.abs(G)
+    if constraint_grad is not None:
+        bA = bA + np.abs(constraint_grad)
+    return bS.reshape(S.shape), rtol * bA
+
+
 __all__ = ["simulate_leaves", "hamming", "int_cost", "random_leaves", "balanced_children",
            "weird_children", "random_topologies", "create_balanced_binary_tree",
            "assert_grad_close", "cond_rtol", "assert_bound_close", "path_dmax", "marginal_rtol",
-           "assert_marginals_close"]
+           "assert_marginals_close", "clear_argmax_mask", "surrogate_grad_bounds"]

@@ -4,8 +4,11 @@ Bars (DESIGN.md "Parity"):
   * hard (tau = 0) DP table, totals, reconstruction, ancestral states:
     bit-exact (integer costs; fp32 values are exact integers);
   * hard gradient (tie-averaged subgradient): rtol 1e-6 vs fp64 oracle;
-  * softmin score / gradient / marginals: rtol 1e-5 vs fp64 oracle
-    (north_star: "grads within 1e-5 for the softmin relaxation").
+  * softmin score / gradient: rtol 1e-5 elementwise vs fp64 oracle
+    (north_star: "grads within 1e-5 for the softmin relaxation");
+  * softmin marginals: elementwise relative, max(1e-5, 8 eps path_dmax /
+    tau) per entry -- fp32 D's conditioning along the entry's root path
+    (tests/_cases.py marginal_rtol; 1e-5 wherever that is below it).
 """
 
 from __future__ import annotations
@@ -14,8 +17,9 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_grad_close, balanced_children, cond_rtol, hamming, int_cost,
-                    random_leaves, random_topologies, simulate_leaves, weird_children)
+from _cases import (assert_grad_close, assert_marginals_close, balanced_children,
+                    clear_argmax_mask, cond_rtol, hamming, int_cost, random_leaves,
+                    random_topologies, simulate_leaves, weird_children)
 from oracle.sankoff_ref import normalize_leaves, run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref
 from trex_amd import SankoffEngine, TreePlan, run_sankoff, sankoff_value_and_grad
@@ -229,14 +233,12 @@ def test_softmin_fwd_grad_vs_fp64(device, tau, L, n):
                                atol=1e-5)
     dc, mg, anc = eng.backward(lv, c, tau, f.dp, marginals=True, anc_states=True)
     assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
-    # per-site marginals are softmax weights of D/tau: fp32 D carries
-    # ~ulp(|D|) error, amplified by 1/tau -> tolerance ~ 8 eps |D|max / tau
-    mtol = max(2e-5, 8 * 1.2e-7 * np.abs(ref["dp"]).max() / tau)
-    np.testing.assert_allclose(_rows(eng, mg), ref["marginals"], atol=mtol)
-    # soft ancestral states = argmax marginals wherever the top two differ
+    # per-site marginals are products of softmax weights of D / tau along the
+    # root path: elementwise relative, bounded by fp32 D's conditioning
     m = ref["marginals"]
-    top2 = np.sort(m, axis=2)[:, :, -2:, :]
-    clear = (top2[:, :, 1] - top2[:, :, 0]) > 4 * mtol
+    _, rt = assert_marginals_close(_rows(eng, mg), m, ch, ref["dp"], tau)
+    # soft ancestral states = argmax marginals wherever the top two differ
+    clear = clear_argmax_mask(m, rt)
     np.testing.assert_array_equal(anc.cpu().numpy()[clear], m.argmax(axis=2)[clear])
 
 

@@ -1298,15 +1298,24 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
     const int32_t* staged = plan + TREX_PLAN_HEADER_INTS + (int64_t)B * s.ni * 6;
     const int32_t* lanes = staged + (int64_t)B * staged_tree_ints(s.ni);
     if (site_eligible(c, lp_slots)) {
-      // the lane-per-site kernel first (sankoff_site.hip): its prologue
-      // kernel decides the mode on the device and writes a flag (tail of the
-      // workspace) the state-parallel launch below checks
+      // the lane-per-site kernel (sankoff_site.hip) takes the call when the
+      // cost matrix allows the factored softmin -- decided on the device: the
+      // state-parallel kernel runs first, gated (every workgroup checks the
+      // cost range and exits when the site kernel takes the call; workgroup
+      // 0 writes K, K^T and the flag into the workspace tail), then the site
+      // kernel (exits unless the flag is set), then one reduce that sums
+      // whichever kernel's partials the flag names
       char* tail = static_cast<char*>(workspace) + wide_workspace_bytes(B, L, Q);
       int* flag = reinterpret_cast<int*>(tail - 128);
       float* kg = reinterpret_cast<float*>(tail - 3456);  // K and K^T
+      c.site_flag = flag;
+      c.site_kg = kg;
+      if (int e = wide_run(fn, c, /*reduce=*/false)) return e;
       if (int e = site_run(fn, c, lanes, lp_slots, flag, kg)) return e;
-      c.mx_flag = flag;
-      c.mx_tiles = site_tiles(L);
+      return partial_reduce(fn, static_cast<double*>(workspace),
+                            static_cast<double*>(workspace) + (int64_t)B * wide_tiles(L, Q), B,
+                            wide_tiles(L, Q), Q, phase, tree_score, d_cost, stream, nullptr, 0, 0,
+                            1, flag, site_tiles(L));
     }
     if (use_staged(B, L, Q, s.ni, s.nl, phase)) return staged_run(fn, c, staged);
     return wide_run(fn, c);

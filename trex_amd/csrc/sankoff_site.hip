@@ -4,11 +4,12 @@
 // Same semantics as sankoff_wide.hip (trex src/trex/sankoff.py run_dp
 // :24-94, run_sankoff :114-188, the build-defined softmin adjoint) for the
 // factored softmin (K = exp(-(C - cmin) / tau), range(C) / tau <= 40) with
-// exact leaf messages.  A one-block prologue kernel decides the mode from the
-// cost matrix on the device, writes K and a flag into the workspace; the
-// state-parallel kernel launched behind this one exits at once when the flag
-// is set (and serves every other mode), the partial reduce picks this
-// kernel's tiles.
+// exact leaf messages.  The state-parallel kernel, launched first, decides
+// the mode from the cost matrix on the device (every workgroup; it exits
+// when this kernel takes the call, and serves every other mode) and its
+// workgroup 0 writes K, K^T and a flag into the workspace (wide_dev.h
+// site_gate_write); this kernel exits unless the flag is set, and the
+// partial reduce picks this kernel's tiles.
 //
 // Mapping.  A work item is one tree x 64 sites, a workgroup of 8 waves; lane
 // = site, a lane keeps all Q states of a vector in registers.  The per-site
@@ -45,7 +46,7 @@ namespace trex {
 
 namespace {
 
-constexpr int kSQ = 20;                    // states per lane (Q padded to 20)
+constexpr int kSQ = kSiteSQ;               // states per lane (Q padded to 20)
 constexpr int kSWv = 8;                    // waves per workgroup
 constexpr int kSlotF = kSQ * kWave;        // floats per slot / scratch vector
 constexpr int kTabF = (kSQ + 1) * kSQ + kSQ;  // leaf messages T[Q + 1][kSQ] + 1 / sum_j K_ij
@@ -68,7 +69,7 @@ struct SiteArgs {
   int8_t* anc;        // [B][n_int][L] or null
   double* part_tree;  // [B * tiles]
   double* part_dc;    // [Q * Q][B * tiles]
-  const float* kg;    // K [kSQ][kSQ] (site_prep_kernel), zero-padded
+  const float* kg;    // K [kSQ][kSQ] and K^T (site_gate_write), zero-padded
   const int* flag;    // 1: this kernel handles the launch
   int n_slots;
 };
@@ -97,28 +98,6 @@ __device__ __forceinline__ void site_barrier() {
 // (4-site groups stay contiguous; 16 rows read at one site group hit 16
 // distinct 16-byte bank groups)
 __device__ __forceinline__ int swz(int i, int s) { return i * kWave + (s ^ ((i & 15) << 2)); }
-
-// One block: the kernel mode from the cost matrix (factored softmin with
-// exact leaf messages), K into the workspace for the scalar loads
-__global__ __launch_bounds__(kWave) void site_prep_kernel(const float* __restrict__ cost, int Q,
-                                                          float a, float* __restrict__ kg,
-                                                          int* __restrict__ flag) {
-  const int lane = threadIdx.x;
-  float lmin = INFINITY, lmax = -INFINITY;
-  for (int e = lane; e < Q * Q; e += kWave) {
-    lmin = fminf(lmin, cost[e]);
-    lmax = fmaxf(lmax, cost[e]);
-  }
-  const float cmin = uniform(wave_minf(lmin)), cmax = uniform(wave_maxf(lmax));
-  const bool handled = use_ktrick(cmin, cmax, a) && (kSentinel - (cmax - cmin)) * a >= 64.0f;
-  for (int e = lane; e < kSQ * kSQ; e += kWave) {
-    const int i = e / kSQ, j = e - i * kSQ;
-    const float kv = (i < Q && j < Q) ? fast_exp2((cmin - cost[i * Q + j]) * a) : 0.0f;
-    kg[e] = kv;                    // K [i][j]
-    kg[kSQ * kSQ + j * kSQ + i] = kv;  // K^T [j][i]
-  }
-  if (lane == 0) flag[0] = handled ? 1 : 0;
-}
 
 // QC: the alphabet size when it is 20 (C3: every state mask folds away), 0 =
 // runtime Q <= 20 with masked padded states
@@ -795,13 +774,12 @@ bool site_eligible(const WideCall& c, int lp_slots) {
   return site_lds_bytes(lp_slots, c.nl, c.ni) <= 160 * 1024;
 }
 
-int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots, int* flag,
-             float* kg) {
+int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots,
+             const int* flag, const float* kg) {
   const int tiles = site_tiles(c.L);
   const size_t lds = site_lds_bytes(lp_slots, c.nl, c.ni);
   if ((int64_t)c.B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
   hipStream_t st = (hipStream_t)c.stream;
-  hipLaunchKernelGGL(site_prep_kernel, dim3(1), dim3(kWave), 0, st, c.cost, c.Q, c.a, kg, flag);
   SiteArgs A;
   A.lanes = lanes;
   A.stride = lp_tree_ints(c.ni);

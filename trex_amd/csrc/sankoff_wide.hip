@@ -52,6 +52,11 @@ struct WArgs {
   const int* ritem;
   int wpi;
   const int* skip = nullptr;  // matrix-core kernel's flag: set -> it handled this launch
+  // gate of the lane-per-site kernel launched behind this one (site_gate_write):
+  // non-null -> decide per workgroup, workgroup 0 writes K / K^T / flag
+  int* site_flag = nullptr;
+  float* site_kg = nullptr;
+  int nitems = 0;  // work items = the grid (partials are [item] / [Q*Q][item])
 };
 
 // LDS map (floats): 4 exchange buffers [4][64], leaf message table
@@ -60,7 +65,8 @@ struct WArgs {
 // (exchange helpers, wmsg / wadj: wide_dev.h)
 
 template <int G, int MODE, int PHASE, bool LFAST, bool SYM, bool RAGGED>
-__device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in, float* lds) {
+__device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in, float* lds,
+                                          const int blk) {
   constexpr bool SOFT = MODE != kHard;
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
@@ -81,8 +87,8 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
   const int* steps;
   int in_item = SPW;  // groups of this wave inside the item
   if constexpr (RAGGED) {
-    const int item = blockIdx.x / A.wpi;
-    const int sub = blockIdx.x - item * A.wpi;
+    const int item = blk / A.wpi;
+    const int sub = blk - item * A.wpi;
     tree = as_const(A.ritem)[item];
     const cptr<int> m = as_const(A.rmeta) + (size_t)tree * kRaggedMeta;
     n_int = m[1];
@@ -95,11 +101,11 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
     rows_base = (size_t)(uint32_t)m[8] | ((size_t)(uint32_t)m[9] << 32);
     steps = A.steps + (size_t)m[0] * 4;
   } else {
-    tree = blockIdx.x / A.tiles;
+    tree = blk / A.tiles;
     n_int = A.n_int;
     nl = A.nl;
     L = A.L;
-    site0 = (blockIdx.x - tree * A.tiles) * SPW;
+    site0 = (blk - tree * A.tiles) * SPW;
     leaf_base = (size_t)tree * nl * L;
     rows_base = (size_t)tree * n_int * L;
     site_base = (size_t)tree * L;
@@ -231,7 +237,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
   if constexpr (FWD) {
     if (leader && A.site_score) A.site_score[site_base + site] = score;
     const double tot = wave_sum(leader ? (double)score : 0.0);
-    if (lane == 0) A.part_tree[blockIdx.x] = tot;
+    if (lane == 0) A.part_tree[blk] = tot;
   }
 
   if constexpr (BWD) {
@@ -316,7 +322,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
     }
 
     // ---- per-wave dC partial: rows i summed over the wave's sites ----
-    const int nb = gridDim.x;
+    const int nb = A.nitems;
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       double v = (double)acc[j];
@@ -325,7 +331,7 @@ __device__ __forceinline__ void wide_body(const WArgs& A, const WCoef<G>& cf_in,
 #pragma unroll
       for (int gq = 1; gq < SPW; ++gq) s += __shfl(v, w.i + gq * G, kWave);
       const int col = acc_col<G, MODE>(w.i, j);
-      if (grp == 0 && !w.pad && col < Q) A.part_dc[(size_t)(w.i * Q + col) * nb + blockIdx.x] = s;
+      if (grp == 0 && !w.pad && col < Q) A.part_dc[(size_t)(w.i * Q + col) * nb + blk] = s;
     }
   }
 }
@@ -335,10 +341,13 @@ __device__ __forceinline__ void wide_dispatch_leaf(const WArgs& A, const WCoef<G
                                                    float* lds) {
   const float range = cmax - cf.cmin;
   const bool lfast = (MODE != kHard) ? ((kSentinel - range) * A.a >= 64.0f) : (range < 99000.0f);
+  // one work item per workgroup (a grid-stride loop here raised the fused
+  // Q = 20 kernel's scratch 56 -> 560 B: SGPR spills into VGPR lanes)
+  const int blk = blockIdx.x;
   if (lfast)
-    wide_body<G, MODE, PHASE, true, SYM, RAGGED>(A, cf, lds);
+    wide_body<G, MODE, PHASE, true, SYM, RAGGED>(A, cf, lds, blk);
   else
-    wide_body<G, MODE, PHASE, false, SYM, RAGGED>(A, cf, lds);
+    wide_body<G, MODE, PHASE, false, SYM, RAGGED>(A, cf, lds, blk);
 }
 
 #ifndef TREX_WIDE_MINW
@@ -358,6 +367,13 @@ __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_
   float cmin, cmax;
   bool sym;
   cost_range<G>(A.cost, Q, i, cmin, cmax, &sym);
+  if constexpr (SOFT && G > 4 && G <= kSiteSQ) {
+    if (A.site_flag) {
+      const bool handled = site_takes_call(cmin, cmax, A.a);
+      if (blockIdx.x == 0) site_gate_write(A.cost, Q, cmin, A.a, A.site_kg, A.site_flag, handled);
+      if (handled) return;
+    }
+  }
   if constexpr (!SOFT) {
     wide_dispatch_leaf<G, kHard, PHASE, RAGGED>(A, make_coefs<G, kHard>(A.cost, Q, i, cmin, A.a), cmax,
                                                 lds);
@@ -737,7 +753,7 @@ int64_t wide_workspace_bytes(int B, int L, int Q) {
   return nb * 8 * (1 + (int64_t)Q * Q) + 3584;
 }
 
-int wide_run(const char* fn, const WideCall& c) {
+int wide_run(const char* fn, const WideCall& c, bool reduce) {
   const int tiles = wide_tiles(c.L, c.Q);
   const size_t lds = wide_lds_bytes(c.n_slots, c.nl, c.ni, c.Q);
   if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
@@ -767,7 +783,10 @@ int wide_run(const char* fn, const WideCall& c) {
   A.ritem = nullptr;
   A.wpi = 0;
   A.skip = c.mx_flag;
+  A.site_flag = c.site_flag;
+  A.site_kg = c.site_kg;
   const int64_t nb = (int64_t)c.B * tiles;
+  A.nitems = (int)nb;
   A.part_tree = static_cast<double*>(c.workspace);
   A.part_dc = A.part_tree + nb;
   hipStream_t st = (hipStream_t)c.stream;
@@ -782,6 +801,7 @@ int wide_run(const char* fn, const WideCall& c) {
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  if (!reduce) return TREX_OK;
   return partial_reduce(fn, A.part_tree, A.part_dc, c.B, tiles, c.Q, c.phase, c.tree_score,
                         c.d_cost, c.stream, nullptr, 0, 0, 1, c.mx_flag, c.mx_tiles);
 }
@@ -826,6 +846,7 @@ int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const i
   A.wpi = wpi;
   A.skip = nullptr;  // ragged batches never run the matrix-core kernel
   const int grid = (int)(items * wpi);
+  A.nitems = grid;
   A.part_tree = static_cast<double*>(c.workspace);
   A.part_dc = A.part_tree + grid;
   hipStream_t st = (hipStream_t)c.stream;

@@ -101,6 +101,11 @@ struct WideCall {
   // exit at once, the reduce sums its mx_tiles partials per tree)
   const int* mx_flag = nullptr;
   int mx_tiles = 0;
+  // gated launch (run_phase): the state-parallel kernel decides per
+  // workgroup whether the lane-per-site kernel takes the call and writes
+  // its K / K^T (site_kg) and the flag (site_flag) from workgroup 0
+  int* site_flag = nullptr;
+  float* site_kg = nullptr;
 };
 constexpr int kWideMaxQ = 64;
 // 64 < Q <= 128: the large-alphabet kernel (sankoff_bigq.hip; int8 leaf codes
@@ -116,7 +121,7 @@ int wide_group(int Q);
 int wide_tiles(int L, int Q);
 size_t wide_lds_bytes(int n_slots, int nl, int ni, int Q);
 int64_t wide_workspace_bytes(int B, int L, int Q);
-int wide_run(const char* fn, const WideCall& c);
+int wide_run(const char* fn, const WideCall& c, bool reduce = true);
 // staged multi-wave kernel (sankoff_staged.hip); staged = the plan's staged
 // regions (after the backtrack entries)
 size_t staged_lds_bytes(int ni, int nl, int Q, int phase);
@@ -140,8 +145,8 @@ int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const i
 // lane-per-site kernel for the factored softmin, 4 < Q <= 20 (sankoff_site.hip)
 bool site_eligible(const WideCall& c, int lp_slots);
 int site_tiles(int L);
-int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots, int* flag,
-             float* kg);
+int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots,
+             const int* flag, const float* kg);
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream);
 int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,

@@ -132,6 +132,29 @@ __device__ __forceinline__ void cost_range(const float* cost, int Q, int i, floa
   if (sym) *sym = __all(s);
 }
 
+// ---- gate of the lane-per-site kernel (sankoff_site.hip, 4 < Q <= 20) ----
+// It takes a soft call when the factored softmin applies and the 1e5
+// sentinel dominates (exact leaf messages); it reads K = exp(-(C - cmin) /
+// tau) [20][20] and K^T with scalar loads.  The state-parallel kernel,
+// launched first, decides this on every workgroup from the cost matrix;
+// its workgroup 0 writes K, K^T and the flag for the site kernel and the
+// reduce launched behind it (no separate prologue launch).
+constexpr int kSiteSQ = 20;
+__device__ __forceinline__ bool site_takes_call(float cmin, float cmax, float a) {
+  return use_ktrick(cmin, cmax, a) && (kSentinel - (cmax - cmin)) * a >= 64.0f;
+}
+__device__ __forceinline__ void site_gate_write(const float* cost, int Q, float cmin, float a,
+                                                float* kg, int* flag, bool handled) {
+  const int lane = threadIdx.x & (kWave - 1);
+  for (int e = lane; e < kSiteSQ * kSiteSQ; e += kWave) {
+    const int i = e / kSiteSQ, j = e - i * kSiteSQ;
+    const float kv = (i < Q && j < Q) ? fast_exp2((cmin - cost[i * Q + j]) * a) : 0.0f;
+    kg[e] = kv;                                  // K [i][j]
+    kg[kSiteSQ * kSiteSQ + j * kSiteSQ + i] = kv;  // K^T [j][i]
+  }
+  if (lane == 0) flag[0] = handled ? 1 : 0;
+}
+
 template <int G>
 __device__ __forceinline__ void xor_perm_coefs(WCoef<G>& cf, int i);
 
