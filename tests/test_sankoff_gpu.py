@@ -41,15 +41,9 @@ def q4_kernel(request, monkeypatch):
     tests/test_configs_full_gpu.py and tests/test_rundp_gpu.py."""
     if request.param == "lane-per-site":
         monkeypatch.setenv("TREX_WIDE_SMALLQ", "0")
-    elif request.param == "state-parallel":
-        monkeypatch.setenv("TREX_WIDE_SMALLQ", "1")
-        monkeypatch.setenv("TREX_STAGED", "0")
-    elif request.param == "staged":
-        monkeypatch.setenv("TREX_WIDE_SMALLQ", "1")
-        monkeypatch.setenv("TREX_STAGED", "1")
     else:
-        monkeypatch.delenv("TREX_WIDE_SMALLQ", raising=False)
-        monkeypatch.delenv("TREX_STAGED", raising=False)
+        monkeypatch.setenv("TREX_WIDE_SMALLQ", "1")
+        monkeypatch.setenv("TREX_STAGED", "1" if request.param == "staged" else "0")
     return request.param
 
 

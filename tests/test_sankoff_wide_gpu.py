@@ -247,10 +247,12 @@ def test_c3_scale_properties(device):
     ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
-    # full-size DP table (elementwise: every D entry is a sum of messages),
+    # full-size DP table (D sums messages of either sign, so entries near 0
+    # carry the absolute error of their terms: rtol 1e-5 with 1e-5 max|D|),
     # marginals and soft ancestral states (the elementwise marginal rule of
     # tests/test_sankoff_gpu.py: fp32 D's conditioning along the root path)
-    assert_grad_close(_sm(f.dp), ref["dp"], rtol=SOFT_RTOL, what="D")
+    np.testing.assert_allclose(_sm(f.dp), ref["dp"], rtol=SOFT_RTOL,
+                               atol=SOFT_RTOL * np.abs(ref["dp"]).max())
     m = ref["marginals"]
     _, rt = assert_marginals_close(_sm(mg), m, ch, ref["dp"], tau)
     clear = clear_argmax_mask(m, rt)

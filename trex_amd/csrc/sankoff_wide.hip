@@ -364,16 +364,26 @@ __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_
   if (A.skip && __hip_atomic_load(A.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int Q = A.Q;
   const int i = threadIdx.x % G;
-  float cmin, cmax;
-  bool sym;
-  cost_range<G>(A.cost, Q, i, cmin, cmax, &sym);
   if constexpr (SOFT && G > 4 && G <= kSiteSQ) {
     if (A.site_flag) {
-      const bool handled = site_takes_call(cmin, cmax, A.a);
-      if (blockIdx.x == 0) site_gate_write(A.cost, Q, cmin, A.a, A.site_kg, A.site_flag, handled);
+      // the gate first, from a lane-parallel pass over C (<= 7 loads per
+      // lane): when the lane-per-site kernel takes the call every workgroup
+      // exits after it
+      float lmin = INFINITY, lmax = -INFINITY;
+      for (int e = threadIdx.x; e < Q * Q; e += kWave) {
+        const float c = A.cost[e];
+        lmin = fminf(lmin, c);
+        lmax = fmaxf(lmax, c);
+      }
+      const float gmin = uniform(wave_minf(lmin)), gmax = uniform(wave_maxf(lmax));
+      const bool handled = site_takes_call(gmin, gmax, A.a);
+      if (blockIdx.x == 0) site_gate_write(A.cost, Q, gmin, A.a, A.site_kg, A.site_flag, handled);
       if (handled) return;
     }
   }
+  float cmin, cmax;
+  bool sym;
+  cost_range<G>(A.cost, Q, i, cmin, cmax, &sym);
   if constexpr (!SOFT) {
     wide_dispatch_leaf<G, kHard, PHASE, RAGGED>(A, make_coefs<G, kHard>(A.cost, Q, i, cmin, A.a), cmax,
                                                 lds);
