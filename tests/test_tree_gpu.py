@@ -229,13 +229,20 @@ def test_tree_optimizer_x3_needs_aligned_rows_and_says_so(device):
     assert opt.gemm == "f32"
 
 
+@pytest.fixture(params=["5", "3"])
+def gram_version(request, monkeypatch):
+    """The x3 Gram kernel: v5 (default) and v3 (TREX_GRAM=3)."""
+    monkeypatch.setenv("TREX_GRAM", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 8192, 128),
-                                      (511, 25000, 256)])
-def test_gram_x3_stays_inside_its_workspace(device, N, K, skip):
+                                      (511, 25000, 256), (511, 200000, 256), (64, 20, 0)])
+def test_gram_x3_stays_inside_its_workspace(device, N, K, skip, gram_version):
     """The split-K Gram writes its partials only inside
     trex_tree_workspace_bytes(N, K) (a guard page of canary bytes after the
     workspace stays untouched) -- for the skipped and un-skipped tile plans,
-    whose split counts differ."""
+    whose split counts differ, and both kernel versions (K = 200 000: C5)."""
     from trex_amd._lib import check, lib, ptr, stream_handle
 
     rng = np.random.default_rng(K + skip)
@@ -344,7 +351,7 @@ def test_gram_skip_keeps_cached_block(device):
 @pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 160, 130),
                                       (100, 1024, 0), (64, 16, 0), (511, 25000, 256),
                                       (300, 1028, 130), (64, 20, 0)])
-def test_split_gram_and_mf_vs_fp64(device, N, K, skip):
+def test_split_gram_and_mf_vs_fp64(device, N, K, skip, gram_version):
     """f16x3 split-product Gram / MF (trex_tree_gram_skip_x3 /
     trex_tree_mf_rows_x3) vs fp64 at the f32 path's bar: softmax-like S
     (values spanning 1e-6 .. 1, one-hot rows) and M = diag(r+c) - (A+A^T)
@@ -412,7 +419,8 @@ def test_adam_seq_step_fused_is_bitwise_separate(device, Q, L):
 
 
 @pytest.mark.parametrize("N,K,skip,x3", [(511, 4096, 0, True), (300, 8192, 128, True),
-                                         (511, 4096, 0, False), (200, 1024, 0, False)])
+                                         (511, 4096, 0, False), (200, 1024, 0, False),
+                                         (511, 200000, 256, True)])
 def test_gram_is_run_to_run_deterministic(device, N, K, skip, x3):
     """The split-K Grams give bitwise the same symmetric G on every run: the
     reduce writes each mirrored pair of a diagonal tile from one thread only

@@ -49,6 +49,13 @@ if __name__ == "__main__":
     tm1 = timed(lambda: check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, N - nl, mx,
                                                                1.0, ptr(cb), cb.numel(), nl, 4,
                                                                ptr(d1), st)))
+    os.environ["TREX_GRAM"] = "3"
+    G3 = torch.zeros((N, N), device=dev)
+    tg3 = timed(lambda: check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, nl, 1.0, ptr(G3), ptr(ws),
+                                                           ws.numel(), st)))
+    os.environ["TREX_GRAM"] = "5"
+    gd = ((G0 - G3).abs()[nl:] / G3.abs()[nl:].clamp_min(1e-30)).max().item()
+    print(f"gram v5 {tg0:.1f} us  gram v3 {tg3:.1f} us  (max rel diff v5 vs v3 {gd:.3g})")
     deq = torch.equal(d0, d1)
     dd = (d0 - d1).abs().max().item()
     print(f"gram {tg0:.1f} us  mf {tm0:.1f} us  mf(codes) {tm1:.1f} us  bitwise dS {deq} "

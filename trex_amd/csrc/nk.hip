@@ -266,6 +266,177 @@ __global__ __launch_bounds__(512) void nk_logits_bwd_kernel(NkArgs a, const floa
   }
 }
 
+// ---- small grids (the reference's eval shape: 32 parents x 15 sites, Q = 2,
+// k = 10: 15 one-wave-per-64-parents blocks, each walking 512 joint states
+// serially, 49 + 78 us) -------------------------------------------------------
+// A block = one site x kNkSmallP parents x kNkSlices slices of the joint index:
+// thread (slice, parent) walks a contiguous range of idx with an odometer,
+// the site's fitness table and the parents' neighbour distributions in LDS;
+// the slices' partial sums combine in fixed slice order.  Same products
+// (left to right over the neighbours, the reference's successive outer
+// products) and prefix / suffix gradients as the kernels above.
+constexpr int kNkSmallThreads = 256;
+constexpr int kNkSlices = 8;
+constexpr int kNkSmallP = kNkSmallThreads / kNkSlices;  // parents per block
+
+struct SmallWalk {
+  int lo, hi;  // joint states [lo, hi) of this thread's slice
+};
+__device__ __forceinline__ SmallWalk small_walk(int QK, int sl) {
+  const int per = (QK + kNkSlices - 1) / kNkSlices;
+  SmallWalk w;
+  w.lo = min(QK, sl * per);
+  w.hi = min(QK, w.lo + per);
+  return w;
+}
+// digits of idx, neighbour 0 most significant
+__device__ __forceinline__ void small_digits(int idx, int k, int Q, int (&d)[kNkMaxK]) {
+#pragma unroll
+  for (int j = kNkMaxK - 1; j >= 0; --j) {
+    if (j < k) {
+      d[j] = idx % Q;
+      idx /= Q;
+    } else {
+      d[j] = 0;
+    }
+  }
+}
+__device__ __forceinline__ void small_next(int (&d)[kNkMaxK], int k, int Q) {
+  for (int j = k - 1; j >= 0; --j) {
+    if (++d[j] < Q) return;
+    d[j] = 0;
+  }
+}
+
+// stage the site's table F [Q][QK] and the block's parents' neighbour
+// distributions P [kNkSmallP][k][Q] into LDS
+__device__ __forceinline__ void small_stage(const NkArgs& a, int site, int p0, float* Fl, float* Pl) {
+  const int QK = a.QK, Q = a.Q, k = a.k;
+  const float* F = a.F + (size_t)site * QK * Q;
+  for (int e = threadIdx.x; e < Q * QK; e += kNkSmallThreads) Fl[e] = F[e];
+  const int32_t* inter = a.inter + (size_t)site * k;
+  for (int e = threadIdx.x; e < kNkSmallP * k * Q; e += kNkSmallThreads) {
+    const int pp = e / (k * Q), jc = e - pp * k * Q, j = jc / Q, c = jc - j * Q;
+    const int r = p0 + pp;
+    Pl[e] = r < a.R ? a.S[((size_t)a.rows[r] * a.L + inter[j]) * Q + c] : 0.0f;
+  }
+}
+
+template <int QT>
+__global__ __launch_bounds__(kNkSmallThreads) void nk_logits_small_kernel(NkArgs a,
+                                                                         float* __restrict__ logits) {
+  constexpr int MQ = QT ? QT : kNkMaxQ;
+  const int Q = QT ? QT : a.Q;
+  const int k = a.k;
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* Fl = sh;                                 // [Q][QK]
+  float* Pl = Fl + (size_t)Q * a.QK;              // [P][k][Q]
+  float* red = Pl + (size_t)kNkSmallP * k * Q;    // [slices][P][Q]
+  const int site = blockIdx.x, p0 = blockIdx.y * kNkSmallP;
+  small_stage(a, site, p0, Fl, Pl);
+  __syncthreads();
+  const int pp = threadIdx.x % kNkSmallP, sl = threadIdx.x / kNkSmallP;
+  const float* P = Pl + (size_t)pp * k * Q;
+  const SmallWalk w = small_walk(a.QK, sl);
+  float acc[MQ];
+#pragma unroll
+  for (int s = 0; s < MQ; ++s) acc[s] = 0.0f;
+  int d[kNkMaxK];
+  small_digits(w.lo, k, Q, d);
+  for (int idx = w.lo; idx < w.hi; ++idx) {
+    float prod = P[d[0]];
+#pragma unroll
+    for (int j = 1; j < kNkMaxK; ++j)
+      if (j < k) prod = prod * P[j * Q + d[j]];
+#pragma unroll
+    for (int s = 0; s < MQ; ++s)
+      if (s < Q) acc[s] = fmaf(Fl[(size_t)s * a.QK + idx], prod, acc[s]);
+    small_next(d, k, Q);
+  }
+#pragma unroll
+  for (int s = 0; s < MQ; ++s)
+    if (s < Q) red[((size_t)sl * kNkSmallP + pp) * Q + s] = acc[s];
+  __syncthreads();
+  const int r = p0 + pp;
+  if (sl != 0 || r >= a.R) return;
+  for (int s = 0; s < Q; ++s) {
+    float v = red[(size_t)pp * Q + s];
+    for (int y = 1; y < kNkSlices; ++y) v += red[((size_t)y * kNkSmallP + pp) * Q + s];
+    logits[((size_t)r * a.L + site) * Q + s] = v;
+  }
+}
+
+template <int QT>
+__global__ __launch_bounds__(kNkSmallThreads) void nk_logits_bwd_small_kernel(
+    NkArgs a, const float* __restrict__ g, float* __restrict__ G) {
+  constexpr int MQ = QT ? QT : kNkMaxQ;
+  const int Q = QT ? QT : a.Q;
+  const int k = a.k, kq = k * Q;
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* Fl = sh;                                     // [Q][QK]
+  float* Pl = Fl + (size_t)Q * a.QK;                  // [P][k][Q]
+  float* gb = Pl + (size_t)kNkSmallP * kq;            // [threads][k][Q] bins
+  const int site = blockIdx.x, p0 = blockIdx.y * kNkSmallP;
+  small_stage(a, site, p0, Fl, Pl);
+  float* bins = gb + (size_t)threadIdx.x * kq;
+  for (int t = 0; t < kq; ++t) bins[t] = 0.0f;
+  __syncthreads();
+  const int pp = threadIdx.x % kNkSmallP, sl = threadIdx.x / kNkSmallP;
+  const int r = p0 + pp;
+  const float* P = Pl + (size_t)pp * kq;
+  float gs[MQ];
+#pragma unroll
+  for (int s = 0; s < MQ; ++s) gs[s] = (s < Q && r < a.R) ? g[((size_t)r * a.L + site) * Q + s] : 0.0f;
+  const SmallWalk w = small_walk(a.QK, sl);
+  int d[kNkMaxK];
+  small_digits(w.lo, k, Q, d);
+  for (int idx = w.lo; idx < w.hi; ++idx) {
+    float dj = 0.0f;
+#pragma unroll
+    for (int s = 0; s < MQ; ++s)
+      if (s < Q) dj = fmaf(gs[s], Fl[(size_t)s * a.QK + idx], dj);
+    float f[kNkMaxK], E[kNkMaxK];
+#pragma unroll
+    for (int j = 0; j < kNkMaxK; ++j) f[j] = j < k ? P[j * Q + d[j]] : 1.0f;
+    float pre = 1.0f;
+#pragma unroll
+    for (int j = 0; j < kNkMaxK; ++j) {
+      E[j] = pre;
+      pre *= f[j];
+    }
+    float suf = 1.0f;
+#pragma unroll
+    for (int j = kNkMaxK - 1; j >= 0; --j) {
+      E[j] *= suf;
+      suf *= f[j];
+    }
+#pragma unroll
+    for (int j = 0; j < kNkMaxK; ++j)
+      if (j < k) bins[j * Q + d[j]] = fmaf(dj, E[j], bins[j * Q + d[j]]);
+    small_next(d, k, Q);
+  }
+  __syncthreads();
+  if (sl != 0 || r >= a.R) return;
+  float* o = G + (((size_t)r * a.L + site) * k) * Q;
+  for (int t = 0; t < kq; ++t) {
+    float v = gb[(size_t)pp * kq + t];
+    for (int y = 1; y < kNkSlices; ++y) v += gb[((size_t)(y * kNkSmallP + pp)) * kq + t];
+    o[t] = v;
+  }
+}
+
+// the small-grid kernels serve grids of few (parent group, site) blocks whose
+// staged table, parents and bins fit 64 KiB of LDS
+size_t nk_small_lds(int Q, int k, int QK, bool bwd) {
+  return ((size_t)Q * QK + (size_t)kNkSmallP * k * Q +
+          (bwd ? (size_t)kNkSmallThreads * k * Q : (size_t)kNkSlices * kNkSmallP * Q)) * 4;
+}
+bool nk_use_small(int R, int L, int Q, int k, int QK) {
+  if (k == 0) return false;
+  const int64_t blocks_wave = (int64_t)((R + kWave - 1) / kWave) * L;
+  return blocks_wave < 256 && nk_small_lds(Q, k, QK, true) <= 65536;
+}
+
 // dS_par [R][L][Q]: for neighbour site m, sum over the (site, j) entries
 // naming m (inverse CSR iofs/ient, ascending (site, j)).  One thread per
 // (r, m, q).
@@ -445,6 +616,16 @@ size_t nk_fwd_lds(int Q, int k, int ns) { return std::max<size_t>(16, ((size_t)k
 size_t nk_bwd_lds(int Q, int k, int ns) { return std::max<size_t>(16, (size_t)(1 + ns) * k * Q * kWave * 4); }
 
 void launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits) {
+  if (nk_use_small(a.R, a.L, a.Q, a.k, a.QK)) {
+    const dim3 sgrid(a.L, (a.R + kNkSmallP - 1) / kNkSmallP);
+    const size_t slds = nk_small_lds(a.Q, a.k, a.QK, false);
+    switch (a.Q) {
+      case 2: hipLaunchKernelGGL(nk_logits_small_kernel<2>, sgrid, dim3(kNkSmallThreads), slds, st, a, logits); break;
+      case 4: hipLaunchKernelGGL(nk_logits_small_kernel<4>, sgrid, dim3(kNkSmallThreads), slds, st, a, logits); break;
+      default: hipLaunchKernelGGL(nk_logits_small_kernel<0>, sgrid, dim3(kNkSmallThreads), slds, st, a, logits);
+    }
+    return;
+  }
   const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);
   const size_t lds = nk_fwd_lds(a.Q, a.k, ns);
   switch (a.Q) {
@@ -456,6 +637,16 @@ void launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits) {
 }
 
 void launch_logits_bwd(const NkArgs& a, int ns, hipStream_t st, const float* g, float* G) {
+  if (nk_use_small(a.R, a.L, a.Q, a.k, a.QK)) {
+    const dim3 sgrid(a.L, (a.R + kNkSmallP - 1) / kNkSmallP);
+    const size_t slds = nk_small_lds(a.Q, a.k, a.QK, true);
+    switch (a.Q) {
+      case 2: hipLaunchKernelGGL(nk_logits_bwd_small_kernel<2>, sgrid, dim3(kNkSmallThreads), slds, st, a, g, G); break;
+      case 4: hipLaunchKernelGGL(nk_logits_bwd_small_kernel<4>, sgrid, dim3(kNkSmallThreads), slds, st, a, g, G); break;
+      default: hipLaunchKernelGGL(nk_logits_bwd_small_kernel<0>, sgrid, dim3(kNkSmallThreads), slds, st, a, g, G);
+    }
+    return;
+  }
   const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);
   const size_t lds = nk_bwd_lds(a.Q, a.k, ns);
   switch (a.Q) {

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "sankoff_dev.h"
 #include "trex_common.h"
@@ -617,6 +618,134 @@ __global__ __launch_bounds__(256) void gram3_reduce_kernel(const float* __restri
   }
 }
 
+// ---- v5 Gram: one wave per SIMD, software-pipelined fragment reads ---------
+// v3's tile enumeration and staging, re-shaped for the MFMA pipe (v3 lost
+// ~60 % of it: every tile's fragments were read right before its MFMAs behind
+// an lgkmcnt(0), and the A-fragment reuse branch split the loop into one
+// basic block per tile).  Here a workgroup is 4 waves (one per SIMD, up to
+// 512 registers: the accumulators live in AGPRs); a wave owns T <= 16
+// consecutive tiles and reads tile t + 1's A / B fragments (4 ds_read_b128)
+// while tile t's three MFMAs run -- no branch anywhere in the chunk body, so
+// the per-row f16 staging of the next chunk and the global loads of the
+// chunk after it are interleaved between the MFMAs (row i of the stage after
+// tile i).  Raw rows are prefetched two chunks ahead (two register sets).
+// A workgroup holds at most 64 tiles, so C5's 100 tiles take two groups; the
+// two groups of a K split sit on the same XCD (blockIdx % 8) and run at the
+// same pace, so the second read of each chunk is an L2 hit.
+constexpr int kG5Waves = 4;
+constexpr int kG5MaxTiles = 16;
+
+template <int T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gram_kernel5(
+    const float* __restrict__ S, int N, int K, int ns, int t0s, int ntiles, int ngroups,
+    int ksplit, int nchunks, float sc, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds5[];
+  const int xcd = blockIdx.x & 7, m = blockIdx.x >> 3;
+  const int g = m % ngroups;
+  const int split = (m / ngroups) * 8 + xcd;
+  if (split >= ksplit) return;
+  const int c_lo = (int)((int64_t)split * nchunks / ksplit);
+  const int c_hi = (int)((int64_t)(split + 1) * nchunks / ksplit);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int tb = (g * kG5Waves + wave) * T;
+  const int nt = max(0, min(T, ntiles - tb));
+  // per-slot strip byte offsets (wave-uniform); slots past the wave's range
+  // repeat the last strips and are not stored
+  int offA[T], offB[T];
+  {
+    int a, b;
+    pair_tiles(min(tb, ntiles - 1), ns, 1, t0s, &a, &b);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      offA[t] = a * (32 * kG3Stride);
+      offB[t] = b * (32 * kG3Stride);
+      const bool wrap = b + 1 >= ns;
+      const int an = wrap ? min(a + 1, ns - 1) : a;
+      b = wrap ? (an > t0s ? an : t0s) : b + 1;
+      a = an;
+    }
+  }
+
+  f32x16 acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = (f32x16){};
+
+  const rsrc_t rs = make_rsrc(S, (uint32_t)((size_t)N * K * 4));
+  const int sub = tid & 3, rb = tid >> 2;
+  constexpr int kRowsPerPass = kG5Waves * kWave / 4;  // 64
+  constexpr int kPasses = kG3Rows / kRowsPerPass;     // 8
+  u32x4 pf[kPasses];
+  auto gload1 = [&](int i, int c) {
+    pf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((rb + kRowsPerPass * i) * K + 4 * sub) * 4,
+                                                  __builtin_amdgcn_readfirstlane(c * 64), 0);
+  };
+  auto stage1 = [&](unsigned char* buf, int i, int c) {
+    const bool kv = 16 * c + 4 * sub < K;
+    g3_stage(buf, rb + kRowsPerPass * i, sub, kv ? pf[i] : (u32x4){0u, 0u, 0u, 0u}, sc);
+  };
+  const int lofs = r * kG3Stride + 16 * h;
+  h8 fa[2][2], fb[2][2];
+  auto rd = [&](const unsigned char* cb, int t, int s) {
+    const unsigned char* pa = cb + offA[t] + lofs;
+    const unsigned char* pb = cb + offB[t] + lofs;
+    fa[s][0] = *reinterpret_cast<const h8*>(pa);
+    fa[s][1] = *reinterpret_cast<const h8*>(pa + 32);
+    fb[s][0] = *reinterpret_cast<const h8*>(pb);
+    fb[s][1] = *reinterpret_cast<const h8*>(pb + 32);
+  };
+
+  if (c_lo < c_hi) {
+#pragma unroll
+    for (int i = 0; i < kPasses; ++i) gload1(i, c_lo);
+#pragma unroll
+    for (int i = 0; i < kPasses; ++i) {
+      stage1(lds5, i, c_lo);
+      gload1(i, c_lo + 1);
+    }
+  }
+  lds_barrier();
+  // chunk c: MFMAs on buf[(c - c_lo) & 1]; stage chunk c + 1 (in pf) into
+  // the other buffer and refill pf with chunk c + 2.  Past the split's last
+  // chunk the stage and loads run on (ignored) neighbouring data: the body
+  // stays branch-free.
+  for (int c = c_lo; c < c_hi; ++c) {
+    const int odd = (c - c_lo) & 1;
+    const unsigned char* cb = lds5 + odd * kG3Buf;
+    unsigned char* nb = lds5 + (odd ^ 1) * kG3Buf;
+    rd(cb, 0, 0);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      if (t + 1 < T) rd(cb, t + 1, (t + 1) & 1);
+      acc[t] = mfma_x3(fa[t & 1][0], fa[t & 1][1], fb[t & 1][0], fb[t & 1][1], acc[t]);
+      if (t < kPasses) {
+        stage1(nb, t, c + 1);
+        gload1(t, c + 2);
+      }
+    }
+#pragma unroll
+    for (int i = T; i < kPasses; ++i) {
+      stage1(nb, i, c + 1);
+      gload1(i, c + 2);
+    }
+    lds_barrier();
+  }
+
+  const float unscale = 1.0f / (sc * sc);
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    if (t < nt) {
+      float* out = part + ((size_t)split * ntiles + tb + t) * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+        out[row * 32 + r] = acc[t][q] * unscale;
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // a9 combine: per row i (one block): rowloss_i, dA row, M row.
 //   loss = sum_ij A_ij (G_ii + G_jj - 2 G_ij) / 2 ; dA_ij = (G_ii+G_jj)/2 - G_ij
@@ -1052,6 +1181,207 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     compute(buf1);
     if (g + 2 < G) stage(buf0, r0);
     load(r0);
+    lds_barrier();
+  }
+}
+
+// ---- v5 MF: one wave per SIMD, pipelined fragment reads --------------------
+// v3's chunking, LDS images and leaf-code stages with Gram v5's structure: a
+// workgroup is 4 waves (one per SIMD, accumulators in AGPRs), wave w owns
+// output rows 64w .. 64w + 63 (two row tiles) x the chunk's TPC column tiles,
+// so each B fragment (4 transposed reads) feeds 2 x 3 MFMAs and each A
+// fragment TPC x 3.  One register set of raw operands: the stage-(s + 1)
+// f16 split and the stage-(s + 2) loads ride between the stage-s MFMAs
+// (one raw item after each column tile), with no branch in the stage body
+// (loads past the split run on neighbouring data or out of bounds: 0, and
+// stage into the buffer nobody reads next).
+template <int TPC, bool CODES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void mf_kernel5(
+    const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
+    int nchunks, float* __restrict__ out, float sm, float sf, const uint8_t* __restrict__ codesR,
+    int lcs) {
+  constexpr int CW = TPC * 32;
+  constexpr int NIT = 32 * (CW / 4);  // F (row, column group) float4 items per stage
+  constexpr int IPT = (NIT + 255) / 256;
+  constexpr int SF = (CW * 2 + 191) / 256 * 256 + 64;  // plane row stride (bytes)
+  constexpr int FPLANE = 32 * SF;
+  constexpr int FBUF = 2 * FPLANE;
+  constexpr int MBUF = 256 * kMfStride;
+  constexpr int BUF = FBUF + MBUF;
+  constexpr int MPT = 8;  // M float4 items per thread: rows tid / 8 + 32 i
+  constexpr int NRAW = IPT + MPT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ldsm5[];
+  const int gx = gridDim.x;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int rbase = blockIdx.y * 256 + wave * 64;
+  // M rows row0 .. row0 + nrows - 1 only: rows past them read out of bounds (0)
+  const rsrc_t rm = make_rsrc(Mm + (size_t)row0 * N, (uint32_t)((size_t)nrows * N * 4));
+  // output rows 0 .. nrows - 1: stores past them are dropped by the bounds check
+  const rsrc_t ro = make_rsrc(out, (uint32_t)((size_t)nrows * K * 4));
+  const rsrc_t rf = make_rsrc(F, (uint32_t)((size_t)N * K * 4));
+  const int Lc = K / 4;
+  const rsrc_t rc = make_rsrc(codesR, (uint32_t)(CODES ? (size_t)Lc * 32 * lcs : 0));
+  static_assert(NIT % 256 == 0, "F items tile the workgroup exactly");
+  int fvb[IPT], lofs[IPT], cvb[IPT];
+#pragma unroll
+  for (int j = 0; j < IPT; ++j) {
+    const int item = tid + 256 * j;
+    const int n = item / (CW / 4), cg = item % (CW / 4);
+    fvb[j] = (n * K + 4 * cg) * 4;
+    lofs[j] = n * SF + 8 * cg;
+    cvb[j] = n * Lc + cg;
+  }
+  const int mseg = tid & 7, mrow = tid >> 3;
+  const int mvb = ((blockIdx.y * 256 + mrow) * N + 4 * mseg) * 4;  // + i * 32 rows
+  const int nst = (N + 31) / 32;
+  const int cnt = blockIdx.x < nchunks ? (nchunks - 1 - (int)blockIdx.x) / gx + 1 : 0;
+  const int G = cnt * nst;
+  if (G == 0) return;
+
+  f32x16 acc[2][TPC];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) acc[u][t] = (f32x16){};
+
+  u32x4 raw[NRAW];
+  uint32_t rcode[CODES ? IPT : 1];
+  // raw item i of (chunk fc, stage fs): F items first, then M.  CODES: a
+  // leaf-code stage's F items come from the code bytes instead -- both loads
+  // are issued, the unused one out of bounds (no memory request), so the
+  // stage body has no branch
+  auto load1 = [&](int i, int fc, int fs) {
+    if (i < IPT) {
+      const bool code = CODES && fs < lcs;
+      const int so = __builtin_amdgcn_readfirstlane(code ? 0x7FFF0000 : (fc * CW + fs * 32 * K) * 4);
+      raw[i] = __builtin_amdgcn_raw_buffer_load_b128(rf, fvb[i], so, 0);
+      if (CODES) {
+        const int sc = __builtin_amdgcn_readfirstlane(code ? fs * 32 * Lc + fc * (CW / 4) : 0x7FFF0000);
+        rcode[i] = __builtin_amdgcn_raw_buffer_load_b8(rc, cvb[i], sc, 0);
+      }
+    } else {
+      raw[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          rm, mvb, __builtin_amdgcn_readfirstlane(fs * 128 + (i - IPT) * 32 * N * 4), 0);
+    }
+  };
+  // one-hot x sf is exact in f16 (sf a power of two <= 2^14): a code item's
+  // hi plane is the one-hot pattern and its lo plane 0, as the f32 rows give
+  auto stage1 = [&](unsigned char* buf, int i, int fs) {
+    if (i < IPT) {
+      float e[4] = {__uint_as_float(raw[i].x), __uint_as_float(raw[i].y),
+                    __uint_as_float(raw[i].z), __uint_as_float(raw[i].w)};
+      if (CODES) {
+        const bool code = fs < lcs;
+        const uint32_t cv = rcode[i] & 0xFFu;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) e[c] = code ? (cv == (uint32_t)c ? 1.0f : 0.0f) : e[c];
+      }
+      h4 hi, lo;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float v = e[c] * sf;
+        hi[c] = (_Float16)v;
+        lo[c] = (_Float16)(v - (float)hi[c]);
+      }
+      *reinterpret_cast<h4*>(buf + lofs[i]) = hi;
+      *reinterpret_cast<h4*>(buf + FPLANE + lofs[i]) = lo;
+    } else {
+      const int mi = i - IPT;
+      const uint32_t e[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+      h4 hi, lo;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float v = (fs * 32 + 4 * mseg + c < N) ? __uint_as_float(e[c]) * sm : 0.0f;
+        hi[c] = (_Float16)v;
+        lo[c] = (_Float16)(v - (float)hi[c]);
+      }
+      unsigned char* row = buf + FBUF + (mrow + 32 * mi) * kMfStride + 8 * mseg;
+      *reinterpret_cast<h4*>(row) = hi;
+      *reinterpret_cast<h4*>(row + 64) = lo;
+    }
+  };
+  const int trk = 8 * (lane >> 5) + ((lane & 15) >> 2);
+  const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const float unscale = 1.0f / (sm * sf);
+
+  // cursors: compute (cc, cs); staged stage = compute + 1; loaded = + 2
+  int cc = blockIdx.x, cs = 0;
+  int sc_ = cs + 1, scc = cc;  // staged-stage cursor
+  if (sc_ == nst) { sc_ = 0; scc += gx; }
+  int lc = scc, ls = sc_ + 1;  // load cursor
+  if (ls == nst) { ls = 0; lc += gx; }
+  unsigned char* buf0 = ldsm5;
+  unsigned char* buf1 = ldsm5 + BUF;
+#pragma unroll
+  for (int i = 0; i < NRAW; ++i) load1(i, cc, cs);
+#pragma unroll
+  for (int i = 0; i < NRAW; ++i) {
+    stage1(buf0, i, cs);
+    load1(i, scc, sc_);
+  }
+  lds_barrier();
+  for (int g = 0; g < G; ++g) {
+    const unsigned char* cb = (g & 1) ? buf1 : buf0;
+    unsigned char* nb = (g & 1) ? buf0 : buf1;
+    const unsigned char* pa = cb + FBUF + (wave * 64 + r) * kMfStride + 16 * h;
+    int item = 0;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      h8 ah[2], al[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        ah[u] = *reinterpret_cast<const h8*>(pa + u * 32 * kMfStride + kk * 32);
+        al[u] = *reinterpret_cast<const h8*>(pa + u * 32 * kMfStride + kk * 32 + 64);
+      }
+#pragma unroll
+      for (int t = 0; t < TPC; ++t) {
+        const int o1 = (kk * 16 + trk) * SF + (t * 32 + trc) * 2;
+        const h8 bh = tr_pair(cb + o1, 4 * SF);
+        const h8 bl = tr_pair(cb + FPLANE + o1, 4 * SF);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u][t] = mfma_x3(ah[u], al[u], bh, bl, acc[u][t]);
+        // one raw item per column tile: staged for stage + 1, refilled for + 2
+        if (item < NRAW) {
+          stage1(nb, item, sc_);
+          load1(item, lc, ls);
+          ++item;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 2 * TPC; i < NRAW; ++i) {
+      stage1(nb, i, sc_);
+      load1(i, lc, ls);
+    }
+    if (++ls == nst) { ls = 0; lc += gx; }
+    if (++sc_ == nst) { sc_ = 0; scc += gx; }
+    if (++cs == nst) {  // chunk done: store its tiles, restart the accumulators
+      // branch-free: columns past K (a ragged last tile) get an out-of-
+      // bounds offset, rows past nrows fall outside the store resource
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int t = 0; t < TPC; ++t) {
+          const int col = cc * CW + t * 32 + r;
+          const int row = rbase + u * 32 + 4 * h;
+          const int vo = (col < K && row < nrows) ? (row * K + col) * 4 : 0x7FFFFFF0;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int dr = (q & 3) + 8 * (q >> 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[u][t][q] * unscale), ro,
+                                                  vo, __builtin_amdgcn_readfirstlane(dr * K * 4), 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < TPC; ++t) acc[u][t] = (f32x16){};
+      cs = 0;
+      cc += gx;
+    }
     lds_barrier();
   }
 }
@@ -1563,6 +1893,22 @@ Gram3Plan gram3_plan(int N, int64_t K, int t0s) {
   g.ksplit = std::max(1, std::min(g.nchunks, std::max(1, 256 / g.ngroups)));
   return g;
 }
+// v5: ngroups = ceil(ntiles / 64), T = tiles per wave; ksplit a multiple of
+// 8 (the XCD pairing of a split's groups), about one workgroup per CU
+Gram3Plan gram5_plan(int N, int64_t K, int t0s, int* T) {
+  Gram3Plan g = gram3_plan(N, K, t0s);
+  g.ngroups = std::max(1, (g.ntiles + kG5Waves * kG5MaxTiles - 1) / (kG5Waves * kG5MaxTiles));
+  *T = std::max(1, (g.ntiles + kG5Waves * g.ngroups - 1) / (kG5Waves * g.ngroups));
+  int ks = std::max(1, 256 / g.ngroups);
+  ks = std::max(8, ks / 8 * 8);
+  g.ksplit = std::max(1, std::min(g.nchunks, ks));
+  return g;
+}
+// v5 by default; TREX_GRAM=3 keeps v3 (A/B timing)
+bool gram5_on() {
+  const char* e = std::getenv("TREX_GRAM");
+  return !(e && std::atoi(e) == 3);
+}
 bool gram3_ok(int N, int64_t K) { return N <= kG3Rows && K % 4 == 0 && (int64_t)N * K * 4 < 0x7FFFFFF0LL; }
 }  // namespace
 
@@ -1579,8 +1925,9 @@ int64_t part_bytes(int N, int64_t K) {
     // mean fewer groups and so more splits
     const int ns = (N + 31) / 32;
     for (int t0s = 0; t0s <= ns; ++t0s) {
-      const Gram3Plan g = gram3_plan(N, K, t0s);
-      b = std::max<int64_t>(b, (int64_t)g.ksplit * g.ntiles * 4096);
+      int T5;
+      for (const Gram3Plan& g : {gram3_plan(N, K, t0s), gram5_plan(N, K, t0s, &T5)})
+        b = std::max<int64_t>(b, (int64_t)g.ksplit * g.ntiles * 4096);
     }
   }
   return b;
@@ -1611,7 +1958,9 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
   if (symmetric && X == Y && x3_max > 0.0f && gram3_ok(N, K)) {
-    const Gram3Plan p = gram3_plan(N, K, 2 * t0);
+    int T5 = 0;
+    const bool v5 = gram5_on();
+    const Gram3Plan p = v5 ? gram5_plan(N, K, 2 * t0, &T5) : gram3_plan(N, K, 2 * t0);
     if (p.ntiles == 0) return TREX_OK;
     static bool lds_set = false;
     if (!lds_set) {
@@ -1619,9 +1968,35 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
       lds_set = true;
     }
-    hipLaunchKernelGGL(gram_kernel3, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds, st, X, N,
-                       (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks,
-                       split_scale(x3_max), part);
+    const float sc = split_scale(x3_max);
+    if (v5) {
+      const dim3 grid(((p.ksplit + 7) / 8 * 8) * p.ngroups);
+      static const bool set5 = [] {
+        for (const void* f : {reinterpret_cast<const void*>(gram_kernel5<4>),
+                              reinterpret_cast<const void*>(gram_kernel5<8>),
+                              reinterpret_cast<const void*>(gram_kernel5<10>),
+                              reinterpret_cast<const void*>(gram_kernel5<12>),
+                              reinterpret_cast<const void*>(gram_kernel5<13>),
+                              reinterpret_cast<const void*>(gram_kernel5<16>)})
+          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
+        return true;
+      }();
+      (void)set5;
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(kG5Waves * kWave), kG3Lds, st, X, N, (int)K, p.ns,
+                           p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks, sc, part);
+      };
+      if (T5 <= 4) go(gram_kernel5<4>);
+      else if (T5 <= 8) go(gram_kernel5<8>);
+      else if (T5 <= 10) go(gram_kernel5<10>);
+      else if (T5 <= 12) go(gram_kernel5<12>);
+      else if (T5 <= 13) go(gram_kernel5<13>);
+      else go(gram_kernel5<16>);
+    } else {
+      hipLaunchKernelGGL(gram_kernel3, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds,
+                         st, X, N, (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks,
+                         sc, part);
+    }
     hipLaunchKernelGGL(gram3_reduce_kernel, dim3(p.ntiles * 16), dim3(256), 0, st, part, N, p.ns,
                        p.t0s, p.ntiles, p.ksplit, G);
     return tree_hip_check("gram");
@@ -2018,6 +2393,26 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
   };
   const int lds = 2 * (2 * 32 * 320 + 256 * kMfStride);
   const bool codes = codesR && lcs > 0;
+  const char* ev = std::getenv("TREX_MF");
+  if (!(ev && std::atoi(ev) == 3)) {  // v5 (default); TREX_MF=3 keeps v3
+    auto go5 = [&](auto kernel, int tpc) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      const int nch = (int)((ct + tpc - 1) / tpc);
+      const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
+      hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(256), lds, (hipStream_t)stream, M, S, N,
+                         (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
+                         split_scale(max_abs_s), codesR, lcs);
+    };
+    if (best == 5) {
+      if (codes) go5(mf_kernel5<5, true>, 5);
+      else go5(mf_kernel5<5, false>, 5);
+    } else {
+      if (codes) go5(mf_kernel5<4, true>, 4);
+      else go5(mf_kernel5<4, false>, 4);
+    }
+    return tree_hip_check(fn);
+  }
   if (best == 5) {
     if (codes) go(mf_kernel3<5, true>, 5, lds);
     else go(mf_kernel3<5, false>, 5, lds);

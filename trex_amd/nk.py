@@ -141,6 +141,7 @@ class LandscapeAwareLoss:
         self.plan = torch.as_tensor(plan).to(dev)
         f32 = dict(dtype=torch.float32, device=dev)
         self.S = torch.empty((self.N, self.L, self.Q), **f32)
+        self._s_key = None
         self.dS = torch.empty_like(self.S)
         self.dS_sur = torch.empty_like(self.S)
         self.loss = torch.zeros((1,), **f32)
@@ -164,7 +165,14 @@ class LandscapeAwareLoss:
         n_anc = self.N - self.n_leaves
         if tuple(anc.shape) != (n_anc, self.L, self.Q):
             raise ValueError(f"ancestors must be {(n_anc, self.L, self.Q)}")
-        self.S.copy_(_f32(masked_sequences, dev))
+        # S = masked_sequences with the ancestor rows rewritten below: the
+        # copy is needed only when the caller's tensor changed (torch's
+        # version counter tracks in-place writes; the leaf rows are data)
+        ms = _f32(masked_sequences, dev)
+        key = (ms.data_ptr(), getattr(ms, "_version", None), tuple(ms.shape))
+        if key != self._s_key or key[1] is None:
+            self.S.copy_(ms)
+            self._s_key = key
         check(L_.trex_tree_update_seq(ptr(anc), n_anc, self.L, self.Q, self.T,
                                       ptr(self.S[self.n_leaves:]), st))
         K = self.L * self.Q
