@@ -130,6 +130,29 @@ def test_landscape_loss_deterministic(device):
     assert torch.equal(l1, l2) and torch.equal(g1, g2)
 
 
+def test_landscape_loss_follows_masked_sequence_updates(device):
+    """The loss caches its copy of masked_sequences between calls: writing
+    into the same tensor, or passing another one, must reach the result
+    (the cache keys on the tensor object and torch's version counter)."""
+    c = _case(8, 20, 4, 2, seed=5)
+    land = NK.NKLandscape(c["inter"], c["F"], 4, device)
+    fn = NK.LandscapeAwareLoss(c["A"], 8, land, 0.7, 2)
+    a = torch.as_tensor(c["anc"], device=device)
+    s = torch.as_tensor(c["S0"], device=device)
+    alt = c["S0"].copy()
+    alt[:8] = np.roll(alt[:8], 1, axis=-1)  # every leaf's state changed
+    l0 = float(fn.value_and_grad(a, s)[0][0])
+    s.copy_(torch.as_tensor(alt, device=device))  # in-place write
+    l1 = float(fn.value_and_grad(a, s)[0][0])
+    l2 = float(fn.value_and_grad(a, torch.as_tensor(c["S0"], device=device))[0][0])
+    r0 = nk.landscape_loss_grad(c["anc"].astype(np.float64), c["S0"].astype(np.float64), 8,
+                                c["inter"], c["F"].astype(np.float64), c["A"], 0.7, 2)[0]
+    r1 = nk.landscape_loss_grad(c["anc"].astype(np.float64), alt.astype(np.float64), 8,
+                                c["inter"], c["F"].astype(np.float64), c["A"], 0.7, 2)[0]
+    np.testing.assert_allclose([l0, l1, l2], [r0, r1, r0], rtol=RTOL)
+    assert abs(r1 - r0) > 1e-3 * abs(r0)
+
+
 def test_run_landscape_aware_adam_matches_oracle_loop(device):
     """A few Adam steps on device vs the same loop on the oracle (optax adam
     semantics, tree_ref.adam_step), then argmax reconstruction."""

@@ -231,9 +231,41 @@ def test_tree_optimizer_x3_needs_aligned_rows_and_says_so(device):
 
 @pytest.fixture(params=["5", "3"])
 def gram_version(request, monkeypatch):
-    """The x3 Gram kernel: v5 (default) and v3 (TREX_GRAM=3)."""
+    """The x3 Gram / MF kernels: v5 (default) and v3 (TREX_GRAM=3, TREX_MF=3)."""
     monkeypatch.setenv("TREX_GRAM", request.param)
+    monkeypatch.setenv("TREX_MF", request.param)
     return request.param
+
+
+@pytest.mark.parametrize("N,L,r0", [(511, 1001, 256), (300, 257, 0), (64, 5, 0)])
+def test_mf_v5_is_bitwise_v3(device, N, L, r0, monkeypatch):
+    """MF v5 (one wave per SIMD) keeps v3's per-tile MFMA order (stages,
+    then the two k-steps, f16x3 products in the same order): dS bitwise
+    equal, with and without leaf codes."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    S_np, nl = _onehot_case(N, L, N + L)
+    K = L * 4
+    rng = np.random.default_rng(L)
+    M = _t(rng.normal(size=(N, N)) * 20, device)
+    S = _t(S_np, device)
+    st = stream_handle(torch.device(device))
+    cb = torch.empty(int(lib().trex_tree_leaf_codes_bytes(nl, L)), dtype=torch.uint8, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    check(lib().trex_tree_leaf_codes(ptr(S), nl, L, 4, ptr(cb), cb.numel(), ptr(status), st))
+    mx = float(M.abs().max()) * 1.01
+    outs = {}
+    for ver in ("3", "5"):
+        monkeypatch.setenv("TREX_MF", ver)
+        a = torch.empty((N - r0, K), device=device)
+        b = torch.empty((N - r0, K), device=device)
+        check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, r0, N - r0, mx, 1.0, ptr(a), st))
+        check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, r0, N - r0, mx, 1.0, ptr(cb),
+                                               cb.numel(), nl, 4, ptr(b), st))
+        outs[ver] = (a, b)
+    assert torch.equal(outs["5"][0], outs["3"][0])
+    assert torch.equal(outs["5"][1], outs["3"][1])
+    assert torch.equal(outs["5"][0], outs["5"][1])
 
 
 @pytest.mark.parametrize("N,K,skip", [(511, 4096, 256), (511, 4096, 0), (300, 8192, 128),

@@ -54,6 +54,31 @@ if __name__ == "__main__":
     tg3 = timed(lambda: check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, nl, 1.0, ptr(G3), ptr(ws),
                                                            ws.numel(), st)))
     os.environ["TREX_GRAM"] = "5"
+    os.environ["TREX_MF"] = "3"
+    d3 = torch.empty((N - nl, K), device=dev)
+    tm3 = timed(lambda: check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, N - nl, mx,
+                                                               1.0, ptr(cb), cb.numel(), nl, 4,
+                                                               ptr(d3), st)))
+    os.environ["TREX_MF"] = "5"
+    print(f"mf(codes) v3 {tm3:.1f} us  bitwise v5 == v3 {torch.equal(d1, d3)}")
+    # exact f32 GEMMs (TreeOptimizer(gemm="f32")): v5 against the older kernels
+    f32 = {}
+    for ver in ("5", "3"):
+        os.environ["TREX_GRAM"] = ver
+        os.environ["TREX_MF"] = ver
+        Gf = torch.zeros((N, N), device=dev)
+        df = torch.empty((N - nl, K), device=dev)
+        tg = timed(lambda: check(lib().trex_tree_gram_skip(ptr(S), N, K, nl, ptr(Gf), ptr(ws),
+                                                           ws.numel(), st)))
+        tm = timed(lambda: check(lib().trex_tree_mf_rows(ptr(M), ptr(S), N, K, nl, N - nl,
+                                                         ptr(df), st)))
+        f32[ver] = (tg, tm, Gf, df)
+    os.environ["TREX_GRAM"] = "5"
+    os.environ["TREX_MF"] = "5"
+    gr = ((f32["5"][2] - f32["3"][2]).abs()[nl:] / f32["3"][2].abs()[nl:].clamp_min(1e-30)).max()
+    mr = ((f32["5"][3] - f32["3"][3]).abs() / (M[nl:].abs() @ S.abs()).clamp_min(1e-30)).max()
+    print(f"f32 gram v5 {f32['5'][0]:.1f} us  v3 {f32['3'][0]:.1f} us (max rel diff {gr.item():.3g}); "
+          f"f32 mf v5 {f32['5'][1]:.1f} us  old {f32['3'][1]:.1f} us (max diff / |M||S| {mr.item():.3g})")
     gd = ((G0 - G3).abs()[nl:] / G3.abs()[nl:].clamp_min(1e-30)).max().item()
     print(f"gram v5 {tg0:.1f} us  gram v3 {tg3:.1f} us  (max rel diff v5 vs v3 {gd:.3g})")
     deq = torch.equal(d0, d1)

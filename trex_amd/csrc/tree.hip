@@ -628,14 +628,20 @@ __global__ __launch_bounds__(256) void gram3_reduce_kernel(const float* __restri
 // while tile t's three MFMAs run -- no branch anywhere in the chunk body, so
 // the per-row f16 staging of the next chunk and the global loads of the
 // chunk after it are interleaved between the MFMAs (row i of the stage after
-// tile i).  Raw rows are prefetched two chunks ahead (two register sets).
+// tile i; raw rows one chunk ahead in registers).
 // A workgroup holds at most 64 tiles, so C5's 100 tiles take two groups; the
 // two groups of a K split sit on the same XCD (blockIdx % 8) and run at the
 // same pace, so the second read of each chunk is an L2 hit.
+// X3 = false: the exact f32 Gram on v_mfma_f32_32x32x2_f32 -- rows staged as
+// f32 (the same 80-B row stride), a lane's 8 k of a fragment (k = 8h .. 8h +
+// 7) read as two float4 and fed to 8 MFMAs (MFMA t covers k = t and 8 + t on
+// the two lane halves: the same permutation for both operands).
 constexpr int kG5Waves = 4;
 constexpr int kG5MaxTiles = 16;
 
-template <int T>
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+template <int T, bool X3>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gram_kernel5(
     const float* __restrict__ S, int N, int K, int ns, int t0s, int ntiles, int ngroups,
     int ksplit, int nchunks, float sc, float* __restrict__ part) {
@@ -683,17 +689,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
   auto stage1 = [&](unsigned char* buf, int i, int c) {
     const bool kv = 16 * c + 4 * sub < K;
-    g3_stage(buf, rb + kRowsPerPass * i, sub, kv ? pf[i] : (u32x4){0u, 0u, 0u, 0u}, sc);
+    const u32x4 w = kv ? pf[i] : (u32x4){0u, 0u, 0u, 0u};
+    if constexpr (X3)
+      g3_stage(buf, rb + kRowsPerPass * i, sub, w, sc);
+    else
+      *reinterpret_cast<u32x4*>(buf + (rb + kRowsPerPass * i) * kG3Stride + 16 * sub) = w;
   };
-  const int lofs = r * kG3Stride + 16 * h;
+  const int lofs = r * kG3Stride + (X3 ? 16 : 32) * h;
   h8 fa[2][2], fb[2][2];
+  f32x8 ga[2], gb[2];
   auto rd = [&](const unsigned char* cb, int t, int s) {
     const unsigned char* pa = cb + offA[t] + lofs;
     const unsigned char* pb = cb + offB[t] + lofs;
-    fa[s][0] = *reinterpret_cast<const h8*>(pa);
-    fa[s][1] = *reinterpret_cast<const h8*>(pa + 32);
-    fb[s][0] = *reinterpret_cast<const h8*>(pb);
-    fb[s][1] = *reinterpret_cast<const h8*>(pb + 32);
+    if constexpr (X3) {
+      fa[s][0] = *reinterpret_cast<const h8*>(pa);
+      fa[s][1] = *reinterpret_cast<const h8*>(pa + 32);
+      fb[s][0] = *reinterpret_cast<const h8*>(pb);
+      fb[s][1] = *reinterpret_cast<const h8*>(pb + 32);
+    } else {
+      ga[s] = *reinterpret_cast<const f32x8*>(pa);
+      gb[s] = *reinterpret_cast<const f32x8*>(pb);
+    }
   };
 
   if (c_lo < c_hi) {
@@ -718,7 +734,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       if (t + 1 < T) rd(cb, t + 1, (t + 1) & 1);
-      acc[t] = mfma_x3(fa[t & 1][0], fa[t & 1][1], fb[t & 1][0], fb[t & 1][1], acc[t]);
+      if constexpr (X3) {
+        acc[t] = mfma_x3(fa[t & 1][0], fa[t & 1][1], fb[t & 1][0], fb[t & 1][1], acc[t]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(ga[t & 1][q], gb[t & 1][q], acc[t], 0, 0, 0);
+      }
       if (t < kPasses) {
         stage1(nb, t, c + 1);
         gload1(t, c + 2);
@@ -1195,7 +1217,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // (one raw item after each column tile), with no branch in the stage body
 // (loads past the split run on neighbouring data or out of bounds: 0, and
 // stage into the buffer nobody reads next).
-template <int TPC, bool CODES>
+template <int TPC, bool CODES, bool X3>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void mf_kernel5(
     const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
     int nchunks, float* __restrict__ out, float sm, float sf, const uint8_t* __restrict__ codesR,
@@ -1205,7 +1227,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int IPT = (NIT + 255) / 256;
   constexpr int SF = (CW * 2 + 191) / 256 * 256 + 64;  // plane row stride (bytes)
   constexpr int FPLANE = 32 * SF;
-  constexpr int FBUF = 2 * FPLANE;
+  // X3: f16 hi / lo planes [32 n][SF]; f32: the F slice transposed [CW][32 n]
+  // (144-B columns: a lane's 8 n are two ds_read_b128, conflict-free)
+  constexpr int FBUF = X3 ? 2 * FPLANE : CW * kMfStride;
+  static_assert(X3 || !CODES, "leaf codes ride on the x3 path only");
   constexpr int MBUF = 256 * kMfStride;
   constexpr int BUF = FBUF + MBUF;
   constexpr int MPT = 8;  // M float4 items per thread: rows tid / 8 + 32 i
@@ -1230,7 +1255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int item = tid + 256 * j;
     const int n = item / (CW / 4), cg = item % (CW / 4);
     fvb[j] = (n * K + 4 * cg) * 4;
-    lofs[j] = n * SF + 8 * cg;
+    lofs[j] = X3 ? n * SF + 8 * cg : 4 * cg * kMfStride + 4 * n;
     cvb[j] = n * Lc + cg;
   }
   const int mseg = tid & 7, mrow = tid >> 3;
@@ -1278,6 +1303,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int c = 0; c < 4; ++c) e[c] = code ? (cv == (uint32_t)c ? 1.0f : 0.0f) : e[c];
       }
+      if constexpr (!X3) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) *reinterpret_cast<float*>(buf + lofs[i] + c * kMfStride) = e[c];
+        return;
+      }
       h4 hi, lo;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -1290,6 +1320,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     } else {
       const int mi = i - IPT;
       const uint32_t e[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+      if constexpr (!X3) {
+        float4 v;
+        v.x = (fs * 32 + 4 * mseg < N) ? __uint_as_float(e[0]) : 0.0f;
+        v.y = (fs * 32 + 4 * mseg + 1 < N) ? __uint_as_float(e[1]) : 0.0f;
+        v.z = (fs * 32 + 4 * mseg + 2 < N) ? __uint_as_float(e[2]) : 0.0f;
+        v.w = (fs * 32 + 4 * mseg + 3 < N) ? __uint_as_float(e[3]) : 0.0f;
+        *reinterpret_cast<float4*>(buf + FBUF + (mrow + 32 * mi) * kMfStride + 16 * mseg) = v;
+        return;
+      }
       h4 hi, lo;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -1304,7 +1343,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
   const int trk = 8 * (lane >> 5) + ((lane & 15) >> 2);
   const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  const float unscale = 1.0f / (sm * sf);
+  const float unscale = X3 ? 1.0f / (sm * sf) : 1.0f;
 
   // cursors: compute (cc, cs); staged stage = compute + 1; loaded = + 2
   int cc = blockIdx.x, cs = 0;
@@ -1330,18 +1369,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       h8 ah[2], al[2];
+      f32x8 fa[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        ah[u] = *reinterpret_cast<const h8*>(pa + u * 32 * kMfStride + kk * 32);
-        al[u] = *reinterpret_cast<const h8*>(pa + u * 32 * kMfStride + kk * 32 + 64);
+        if constexpr (X3) {
+          ah[u] = *reinterpret_cast<const h8*>(pa + u * 32 * kMfStride + kk * 32);
+          al[u] = *reinterpret_cast<const h8*>(pa + u * 32 * kMfStride + kk * 32 + 64);
+        } else {  // n = 16 kk + 8 h .. + 7 (pa carries 16 h bytes: one more 16 h)
+          fa[u] = *reinterpret_cast<const f32x8*>(pa + u * 32 * kMfStride + kk * 64 + 16 * h);
+        }
       }
 #pragma unroll
       for (int t = 0; t < TPC; ++t) {
-        const int o1 = (kk * 16 + trk) * SF + (t * 32 + trc) * 2;
-        const h8 bh = tr_pair(cb + o1, 4 * SF);
-        const h8 bl = tr_pair(cb + FPLANE + o1, 4 * SF);
+        if constexpr (X3) {
+          const int o1 = (kk * 16 + trk) * SF + (t * 32 + trc) * 2;
+          const h8 bh = tr_pair(cb + o1, 4 * SF);
+          const h8 bl = tr_pair(cb + FPLANE + o1, 4 * SF);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) acc[u][t] = mfma_x3(ah[u], al[u], bh, bl, acc[u][t]);
+          for (int u = 0; u < 2; ++u) acc[u][t] = mfma_x3(ah[u], al[u], bh, bl, acc[u][t]);
+        } else {
+          // MFMA q covers n = 16 kk + q and 16 kk + 8 + q on the two lane halves
+          const f32x8 fb = *reinterpret_cast<const f32x8*>(cb + (t * 32 + r) * kMfStride + kk * 64 + 32 * h);
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[u][q], fb[q], acc[u][t], 0, 0, 0);
+        }
         // one raw item per column tile: staged for stage + 1, refilled for + 2
         if (item < NRAW) {
           stage1(nb, item, sc_);
@@ -1957,7 +2011,9 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
   if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
-  if (symmetric && X == Y && x3_max > 0.0f && gram3_ok(N, K)) {
+  // v5 serves both precisions; v3 (TREX_GRAM=3) only the x3 one
+  const bool x3 = x3_max > 0.0f;
+  if (symmetric && X == Y && gram3_ok(N, K) && (x3 || gram5_on())) {
     int T5 = 0;
     const bool v5 = gram5_on();
     const Gram3Plan p = v5 ? gram5_plan(N, K, 2 * t0, &T5) : gram3_plan(N, K, 2 * t0);
@@ -1968,30 +2024,45 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
       lds_set = true;
     }
-    const float sc = split_scale(x3_max);
+    const float sc = x3 ? split_scale(x3_max) : 1.0f;
     if (v5) {
       const dim3 grid(((p.ksplit + 7) / 8 * 8) * p.ngroups);
       static const bool set5 = [] {
-        for (const void* f : {reinterpret_cast<const void*>(gram_kernel5<4>),
-                              reinterpret_cast<const void*>(gram_kernel5<8>),
-                              reinterpret_cast<const void*>(gram_kernel5<10>),
-                              reinterpret_cast<const void*>(gram_kernel5<12>),
-                              reinterpret_cast<const void*>(gram_kernel5<13>),
-                              reinterpret_cast<const void*>(gram_kernel5<16>)})
+        for (const void* f : {reinterpret_cast<const void*>(gram_kernel5<4, true>),
+                              reinterpret_cast<const void*>(gram_kernel5<8, true>),
+                              reinterpret_cast<const void*>(gram_kernel5<10, true>),
+                              reinterpret_cast<const void*>(gram_kernel5<12, true>),
+                              reinterpret_cast<const void*>(gram_kernel5<13, true>),
+                              reinterpret_cast<const void*>(gram_kernel5<16, true>),
+                              reinterpret_cast<const void*>(gram_kernel5<4, false>),
+                              reinterpret_cast<const void*>(gram_kernel5<8, false>),
+                              reinterpret_cast<const void*>(gram_kernel5<10, false>),
+                              reinterpret_cast<const void*>(gram_kernel5<12, false>),
+                              reinterpret_cast<const void*>(gram_kernel5<13, false>),
+                              reinterpret_cast<const void*>(gram_kernel5<16, false>)})
           (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
         return true;
       }();
       (void)set5;
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kG5Waves * kWave), kG3Lds, st, X, N, (int)K, p.ns,
-                           p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks, sc, part);
+                           p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks, x3 ? sc : 1.0f, part);
       };
-      if (T5 <= 4) go(gram_kernel5<4>);
-      else if (T5 <= 8) go(gram_kernel5<8>);
-      else if (T5 <= 10) go(gram_kernel5<10>);
-      else if (T5 <= 12) go(gram_kernel5<12>);
-      else if (T5 <= 13) go(gram_kernel5<13>);
-      else go(gram_kernel5<16>);
+      if (x3) {
+        if (T5 <= 4) go(gram_kernel5<4, true>);
+        else if (T5 <= 8) go(gram_kernel5<8, true>);
+        else if (T5 <= 10) go(gram_kernel5<10, true>);
+        else if (T5 <= 12) go(gram_kernel5<12, true>);
+        else if (T5 <= 13) go(gram_kernel5<13, true>);
+        else go(gram_kernel5<16, true>);
+      } else {
+        if (T5 <= 4) go(gram_kernel5<4, false>);
+        else if (T5 <= 8) go(gram_kernel5<8, false>);
+        else if (T5 <= 10) go(gram_kernel5<10, false>);
+        else if (T5 <= 12) go(gram_kernel5<12, false>);
+        else if (T5 <= 13) go(gram_kernel5<13, false>);
+        else go(gram_kernel5<16, false>);
+      }
     } else {
       hipLaunchKernelGGL(gram_kernel3, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds,
                          st, X, N, (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks,
@@ -2340,6 +2411,11 @@ extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N
   return tree_hip_check("trex_tree_surrogate_combine");
 }
 
+namespace {
+int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int row0, int nrows,
+          float max_abs_m, float max_abs_s, float* dS_rows, const uint8_t* codesR, int lcs,
+          void* stream, bool x3);
+}  // namespace
 extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t K, int row0,
                                  int nrows, float* dS_rows, void* stream) {
   if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
@@ -2347,6 +2423,12 @@ extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t 
     return set_error(TREX_E_ARG, "trex_tree_mf_rows: bad arguments");
   if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
     return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows: S exceeds 2 GiB");
+  // v5 f32 (one wave per SIMD, K % 4 == 0: 16-B rows); TREX_MF=3 or a
+  // ragged K: the one-wave-per-tile kernel
+  const char* ev = std::getenv("TREX_MF");
+  if (K % 4 == 0 && !(ev && std::atoi(ev) == 3))
+    return mf_x3("trex_tree_mf_rows", M, S, N, K, row0, nrows, 1.0f, 1.0f, dS_rows, nullptr, 0,
+                 stream, false);
   const int nrowt = (nrows + 63) / 64;
   const int ncolb = (int)((K + 63) / 64);
   const int blocks = nrowt * ((ncolb + 7) / 8 * 8);
@@ -2359,7 +2441,7 @@ namespace {
 // v3 MF launch; codesR / lcs: leaf-code stages (CODES instantiation) or null / 0
 int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int row0, int nrows,
           float max_abs_m, float max_abs_s, float* dS_rows, const uint8_t* codesR, int lcs,
-          void* stream) {
+          void* stream, bool x3) {
   if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
       row0 + nrows > N || !pos_finite_f32(max_abs_m) || !pos_finite_f32(max_abs_s))
     return set_error(TREX_E_ARG, "%s: bad arguments", fn);
@@ -2394,22 +2476,27 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
   const int lds = 2 * (2 * 32 * 320 + 256 * kMfStride);
   const bool codes = codesR && lcs > 0;
   const char* ev = std::getenv("TREX_MF");
-  if (!(ev && std::atoi(ev) == 3)) {  // v5 (default); TREX_MF=3 keeps v3
+  if (!x3 || !(ev && std::atoi(ev) == 3)) {  // v5 (default); TREX_MF=3 keeps v3 (x3 only)
+    // f32: the transposed F slice is CW x 144 B
+    const int lds5 = x3 ? lds : 2 * (160 * kMfStride + 256 * kMfStride);
     auto go5 = [&](auto kernel, int tpc) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds5);
       const int nch = (int)((ct + tpc - 1) / tpc);
       const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
-      hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(256), lds, (hipStream_t)stream, M, S, N,
-                         (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
-                         split_scale(max_abs_s), codesR, lcs);
+      hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(256), lds5, (hipStream_t)stream, M, S, N,
+                         (int)K, row0, nrows, nch, dS_rows, x3 ? split_scale(max_abs_m) : 1.0f,
+                         x3 ? split_scale(max_abs_s) : 1.0f, codesR, lcs);
     };
-    if (best == 5) {
-      if (codes) go5(mf_kernel5<5, true>, 5);
-      else go5(mf_kernel5<5, false>, 5);
+    if (!x3) {
+      if (best == 5) go5(mf_kernel5<5, false, false>, 5);
+      else go5(mf_kernel5<4, false, false>, 4);
+    } else if (best == 5) {
+      if (codes) go5(mf_kernel5<5, true, true>, 5);
+      else go5(mf_kernel5<5, false, true>, 5);
     } else {
-      if (codes) go5(mf_kernel5<4, true>, 4);
-      else go5(mf_kernel5<4, false>, 4);
+      if (codes) go5(mf_kernel5<4, true, true>, 4);
+      else go5(mf_kernel5<4, false, true>, 4);
     }
     return tree_hip_check(fn);
   }
@@ -2454,7 +2541,7 @@ extern "C" int trex_tree_mf_rows_x3(const float* M, const float* S, int N, int64
                                     int nrows, float max_abs_m, float max_abs_s, float* dS_rows,
                                     void* stream) {
   return mf_x3("trex_tree_mf_rows_x3", M, S, N, K, row0, nrows, max_abs_m, max_abs_s, dS_rows,
-               nullptr, 0, stream);
+               nullptr, 0, stream, true);
 }
 
 extern "C" int trex_tree_leaf_code_rows(int n_leaf) { return n_leaf >= 32 ? 32 * (n_leaf / 32) : 0; }
@@ -2493,7 +2580,7 @@ extern "C" int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N,
     return set_error(TREX_E_ARG, "trex_tree_mf_rows_x3_codes: codes buffer smaller than "
                                  "trex_tree_leaf_codes_bytes(n_leaf, K / Q)");
   return mf_x3("trex_tree_mf_rows_x3_codes", M, S, N, K, row0, nrows, max_abs_m, max_abs_s,
-               dS_rows, static_cast<const uint8_t*>(codes), lcr / 32, stream);
+               dS_rows, static_cast<const uint8_t*>(codes), lcr / 32, stream, true);
 }
 
 extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,

@@ -141,7 +141,7 @@ class LandscapeAwareLoss:
         self.plan = torch.as_tensor(plan).to(dev)
         f32 = dict(dtype=torch.float32, device=dev)
         self.S = torch.empty((self.N, self.L, self.Q), **f32)
-        self._s_key = None
+        self._s_src, self._s_ver = None, None
         self.dS = torch.empty_like(self.S)
         self.dS_sur = torch.empty_like(self.S)
         self.loss = torch.zeros((1,), **f32)
@@ -166,13 +166,14 @@ class LandscapeAwareLoss:
         if tuple(anc.shape) != (n_anc, self.L, self.Q):
             raise ValueError(f"ancestors must be {(n_anc, self.L, self.Q)}")
         # S = masked_sequences with the ancestor rows rewritten below: the
-        # copy is needed only when the caller's tensor changed (torch's
-        # version counter tracks in-place writes; the leaf rows are data)
+        # copy is needed only when the caller passes another tensor or wrote
+        # into this one (torch's version counter); the cached reference keeps
+        # the tensor alive, so its storage cannot be reused under the cache
         ms = _f32(masked_sequences, dev)
-        key = (ms.data_ptr(), getattr(ms, "_version", None), tuple(ms.shape))
-        if key != self._s_key or key[1] is None:
+        ver = getattr(ms, "_version", None)
+        if ms is not self._s_src or ver is None or ver != self._s_ver:
             self.S.copy_(ms)
-            self._s_key = key
+            self._s_src, self._s_ver = ms, ver
         check(L_.trex_tree_update_seq(ptr(anc), n_anc, self.L, self.Q, self.T,
                                       ptr(self.S[self.n_leaves:]), st))
         K = self.L * self.Q
