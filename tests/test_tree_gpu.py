@@ -97,9 +97,10 @@ def test_surrogate_value_and_grads(device, N, L, Q):
                                rtol=RTOL)
 
 
-def test_surrogate_onehot_is_edge_hamming_exact(device):
+@pytest.mark.parametrize("nl,L", [(64, 2000), (16, 60)])  # (16, 60): the one-launch small path
+def test_surrogate_onehot_is_edge_hamming_exact(device, nl, L):
     rng = np.random.default_rng(5)
-    nl, L, Q = 64, 2000, 4
+    Q = 4
     n = 2 * nl - 1
     seq = rng.integers(0, Q, size=(n, L))
     S = np.eye(Q, dtype=np.float32)[seq]

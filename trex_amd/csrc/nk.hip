@@ -20,9 +20,12 @@
 // per-lane LDS block [j][c][lane] (conflict-free) and walks the Q^k joint
 // states.  The reverse sweep re-walks them: dJ[idx] = sum_s g_s F[s][idx],
 // G[j][c_j] += dJ[idx] * prod_{j' != j} P_j'[c_j'] (prefix / suffix products),
-// written per (parent, site, j); a gather kernel then sums G over the
+// written per (parent, site, j); the combine kernel then sums G over the
 // (site, j) pairs that name each neighbour site (inverse-interaction CSR from
-// the host plan) -- fixed order, no atomics, bitwise reproducible.
+// the host plan) -- fixed order, no atomics, bitwise reproducible.  Few
+// parents x sites (the reference's eval shape: 31 x 15) take the small-grid
+// kernels: a block per (site, 32 parents), the joint states split over 8
+// slices of threads and summed in slice order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -437,29 +440,6 @@ bool nk_use_small(int R, int L, int Q, int k, int QK) {
   return blocks_wave < 256 && nk_small_lds(Q, k, QK, true) <= 65536;
 }
 
-// dS_par [R][L][Q]: for neighbour site m, sum over the (site, j) entries
-// naming m (inverse CSR iofs/ient, ascending (site, j)).  One thread per
-// (r, m, q).
-__global__ __launch_bounds__(256) void nk_gather_kernel(const float* __restrict__ G,
-                                                        const int32_t* __restrict__ iofs,
-                                                        const int32_t* __restrict__ ient, int R,
-                                                        int L, int Q, int k,
-                                                        float* __restrict__ dpar) {
-  const int64_t total = (int64_t)R * L * Q;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(t % Q);
-    const int64_t rm = t / Q;
-    const int m = (int)(rm % L);
-    const int64_t r = rm / L;
-    float acc = 0.0f;
-    for (int e = iofs[m]; e < iofs[m + 1]; ++e) {
-      const int lj = ient[e];  // site * k + j
-      acc += G[((size_t)r * L * k + lj) * Q + q];
-    }
-    dpar[t] = acc;
-  }
-}
 
 // Cross-entropy of every child against its parent's logits (benchmark.py
 // :292-300).  One lane per (compact parent pc, site).  Writes
@@ -529,6 +509,7 @@ __global__ __launch_bounds__(256) void nk_ce_kernel(const float* __restrict__ S,
 // sums[b]; nk_loss_kernel then sums the chunks and writes
 // loss = surrogate + lambda * ce / norm
 constexpr int kNkChunks = 256;
+constexpr int64_t kNkDirectParts = 8192;
 __global__ __launch_bounds__(256) void nk_chunk_sum_kernel(const double* __restrict__ part,
                                                            int64_t n, double* __restrict__ sums) {
   __shared__ double red[256];
@@ -561,12 +542,16 @@ __global__ __launch_bounds__(256) void nk_loss_kernel(const double* __restrict__
   if (threadIdx.x == 0) loss[0] = (float)((surrogate ? (double)surrogate[0] : 0.0) + coef * red[0]);
 }
 
-// dS = dS_in + dchild + dpar[rowmap[n]]   (rowmap -1: not a parent)
+// d_seqs = d_seqs_in + dchild + (for a parent row) the gathered per-slot
+// logits gradients: for site m of parent pc, the sum over the inverse-
+// interaction entries of m of G[pc][site][j][q] (trex_nk_plan_build order)
 __global__ __launch_bounds__(256) void nk_combine_kernel(const float* __restrict__ din,
                                                          const float* __restrict__ dchild,
-                                                         const float* __restrict__ dpar,
+                                                         const float* __restrict__ G,
+                                                         const int32_t* __restrict__ iofs,
+                                                         const int32_t* __restrict__ ient,
                                                          const int32_t* __restrict__ rowmap,
-                                                         int N, int L, int Q,
+                                                         int N, int L, int Q, int k,
                                                          float* __restrict__ dout) {
   const int64_t per = (int64_t)L * Q;
   const int64_t total = (int64_t)N * per;
@@ -576,7 +561,15 @@ __global__ __launch_bounds__(256) void nk_combine_kernel(const float* __restrict
     const int64_t w = t - (int64_t)n * per;
     const int pc = rowmap[n];
     float v = (din ? din[t] : 0.0f) + dchild[t];
-    if (pc >= 0) v += dpar[(int64_t)pc * per + w];
+    if (pc >= 0) {
+      float acc = 0.0f;
+      if (G) {
+        const int m = (int)(w / Q), q = (int)(w - (int64_t)m * Q);
+        for (int e = iofs[m]; e < iofs[m + 1]; ++e)
+          acc += G[((size_t)pc * L * k + ient[e]) * Q + q];
+      }
+      v += acc;
+    }
     dout[t] = v;
   }
 }
@@ -830,20 +823,26 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
   hipLaunchKernelGGL(nk_ce_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
                      seqs, logits, v.cofs, v.cidx, seq_mask, n_parents, L, Q, scale, dlog, dchild,
                      part);
-  hipLaunchKernelGGL(nk_chunk_sum_kernel, dim3(kNkChunks), dim3(256), 0, st, part,
-                     (int64_t)n_parents * L, sums);
-  hipLaunchKernelGGL(nk_loss_kernel, dim3(1), dim3(256), 0, st, sums, (int64_t)kNkChunks,
-                     surrogate, (double)lambda_val / norm, loss);
+  // few (parent, site) partials (the eval shape: 465): one block sums them
+  // directly; otherwise two fixed levels (chunks, then the chunk sums)
+  const int64_t nparts = (int64_t)n_parents * L;
+  if (nparts <= kNkDirectParts) {
+    hipLaunchKernelGGL(nk_loss_kernel, dim3(1), dim3(256), 0, st, part, nparts, surrogate,
+                       (double)lambda_val / norm, loss);
+  } else {
+    hipLaunchKernelGGL(nk_chunk_sum_kernel, dim3(kNkChunks), dim3(256), 0, st, part, nparts, sums);
+    hipLaunchKernelGGL(nk_loss_kernel, dim3(1), dim3(256), 0, st, sums, (int64_t)kNkChunks,
+                       surrogate, (double)lambda_val / norm, loss);
+  }
   if (int e = nk_err(fn)) return e;
   if (!d_seqs) return TREX_OK;
-  if (k > 0) {
-    launch_logits_bwd(a, ns, st, dlog, G);
-    hipLaunchKernelGGL(nk_gather_kernel, dim3(grid1d((int64_t)n_parents * per, 256)), dim3(256), 0,
-                       st, G, v.iofs, v.ient, n_parents, L, Q, k, dpar);
-  } else {
-    (void)hipMemsetAsync(dpar, 0, (size_t)n_parents * per * 4, st);
-  }
+  // the per-slot gradients G are gathered into each parent row inline by the
+  // combine: for neighbour site m, the sum over the (site, j) entries naming
+  // m (inverse CSR iofs / ient, ascending (site, j))
+  if (k > 0) launch_logits_bwd(a, ns, st, dlog, G);
+  (void)dpar;
   hipLaunchKernelGGL(nk_combine_kernel, dim3(grid1d((int64_t)N * per, 256)), dim3(256), 0, st,
-                     d_seqs_in, dchild, dpar, v.rowmap, N, L, Q, d_seqs);
+                     d_seqs_in, dchild, k > 0 ? G : nullptr, v.iofs, v.ient, v.rowmap, N, L, Q, k,
+                     d_seqs);
   return nk_err(fn);
 }

@@ -855,6 +855,72 @@ __global__ void step_advance_kernel(StepState* __restrict__ st, float b1, float 
   }
 }
 
+// The whole surrogate for small trees (N <= 64, N K <= 8192: the NK eval
+// shape is 63 x 30) in one workgroup: S, G = S S^T and M in LDS, G by
+// fp32 fmaf over k in order (i <= j computed, mirrored: exactly symmetric),
+// the combine's rows in fp64 (thread i sums row i over j in order), the
+// loss summed over rows in order by thread 0, dS = M S.  One launch where
+// the general path takes five (Gram, its reduce, combine, row sum, MF).
+constexpr int kSurSmallN = 64;
+constexpr int kSurSmallNK = 8192;
+__global__ __launch_bounds__(256) void surrogate_small_kernel(const float* __restrict__ S,
+                                                             const float* __restrict__ A, int N,
+                                                             int K, float* __restrict__ loss,
+                                                             float* __restrict__ dS,
+                                                             float* __restrict__ dA,
+                                                             float* __restrict__ G_out) {
+  __shared__ float sS[kSurSmallNK];
+  __shared__ float sG[kSurSmallN * kSurSmallN];
+  __shared__ float sM[kSurSmallN * kSurSmallN];
+  __shared__ double rl[kSurSmallN];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < N * K; e += 256) sS[e] = S[e];
+  __syncthreads();
+  for (int e = tid; e < N * N; e += 256) {
+    const int i = e / N, j = e - i * N;
+    if (i > j) continue;
+    float g = 0.0f;
+    for (int k = 0; k < K; ++k) g = fmaf(sS[i * K + k], sS[j * K + k], g);
+    sG[i * N + j] = g;
+    sG[j * N + i] = g;
+  }
+  __syncthreads();
+  if (tid < N) {
+    const int i = tid;
+    const float gii = sG[i * N + i];
+    double l = 0.0, rs = 0.0, cs = 0.0;
+    for (int j = 0; j < N; ++j) {
+      const float a = A[(size_t)i * N + j];
+      const float at = A[(size_t)j * N + i];
+      const float gjj = sG[j * N + j];
+      const float gij = sG[i * N + j];
+      l += (double)a * ((double)gii + (double)gjj - 2.0 * (double)gij);
+      rs += a;
+      cs += at;
+      if (dA) dA[(size_t)i * N + j] = 0.5f * (gii + gjj) - gij;
+      sM[i * N + j] = -(a + at);
+    }
+    sM[i * N + i] += (float)(rs + cs);
+    rl[i] = 0.5 * l;
+  }
+  if (G_out)
+    for (int e = tid; e < N * N; e += 256) G_out[e] = sG[e];
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int i = 0; i < N; ++i) t += rl[i];
+    loss[0] = (float)t;
+  }
+  if (dS) {
+    for (int e = tid; e < N * K; e += 256) {
+      const int n = e / K, k = e - n * K;
+      float v = 0.0f;
+      for (int j = 0; j < N; ++j) v = fmaf(sM[n * N + j], sS[j * K + k], v);
+      dS[e] = v;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict__ v, int n,
                                                       float scale, float* __restrict__ out,
                                                       int accumulate,
@@ -2105,6 +2171,11 @@ extern "C" int trex_tree_surrogate(const float* S, const float* A, int N, int64_
   float* M = reinterpret_cast<float*>(w);
   w += (int64_t)N * N * 4;
   double* rowloss = reinterpret_cast<double*>(w);
+  if (N <= kSurSmallN && (int64_t)N * K <= kSurSmallNK) {
+    hipLaunchKernelGGL(surrogate_small_kernel, dim3(1), dim3(256), 0, st, S, A, N, (int)K, loss,
+                       dS, dA, G_out);
+    return tree_hip_check("trex_tree_surrogate");
+  }
   if (int e = gram(S, S, N, K, 1, G, part, st)) return e;
   hipLaunchKernelGGL(surrogate_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, dA,
                      dS ? M : nullptr, rowloss);
