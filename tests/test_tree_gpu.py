@@ -595,3 +595,36 @@ def test_tree_device_loop_is_bitwise_eager(device, gemm, capture):
 
     np.testing.assert_allclose(_n(G.gumbel_noise_step(seed, 3, shape, device)).ravel(),
                                gumbel_noise(seed, 3, shape[0] * shape[1]), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("gemm", ["x3", "f32"])
+def test_tree_optimizer_checkpoint_resume_is_bitwise(device, gemm, tmp_path):
+    """save_checkpoint after 3 steps, load into a fresh TreeOptimizer (same
+    leaves), 3 more steps: losses and parameters bitwise those of the
+    uninterrupted 6-step run (SURVEY.md §5 checkpoint / resume: params and
+    the Adam state; S and the Gram are recomputed)."""
+    params, noise, seqs = _tree_case(16, 52, 4, 23)
+    nz = _t(noise, device)
+    temps = [2.0, 1.8, 1.6, 1.4, 1.2, 1.0, 0.9]
+
+    def make():
+        return G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                               lr=0.02, gemm=gemm)
+
+    ref = make()
+    ref_losses = [float(ref.step(temps[i], nz, temps[i + 1])) for i in range(6)]
+    first = make()
+    for i in range(3):
+        first.step(temps[i], nz, temps[i + 1])
+    path = tmp_path / "c5.npz"
+    first.save_checkpoint(path)
+    resumed = make()
+    resumed.load_checkpoint(path)
+    assert resumed.opt.count == 3
+    losses = [float(resumed.step(temps[i], nz, temps[i + 1])) for i in range(3, 6)]
+    assert losses == ref_losses[3:]
+    for k in ref.params:
+        assert torch.equal(resumed.params[k], ref.params[k]), k
+    for k in ref.opt.mu:
+        assert torch.equal(resumed.opt.mu[k], ref.opt.mu[k]) and torch.equal(resumed.opt.nu[k],
+                                                                            ref.opt.nu[k]), k

@@ -21,6 +21,8 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
+
 from ._lib import check, lib, ptr, stream_handle
 
 
@@ -295,6 +297,25 @@ class Adam:
         # the right count (trex_step_advance; bitwise the host-count update)
         self.state = step_state(dev)
 
+    def state_dict(self) -> dict:
+        """Host copies of the optimiser state: step count, first / second
+        moments (optax's ScaleByAdamState)."""
+        return {"count": int(self.count),
+                "mu": {k: v.detach().cpu().clone() for k, v in self.mu.items()},
+                "nu": {k: v.detach().cpu().clone() for k, v in self.nu.items()}}
+
+    def load_state_dict(self, sd: dict):
+        """Restore a ``state_dict``; the device step record restarts at its
+        count (the next step recomputes the bias corrections from it)."""
+        for name in ("mu", "nu"):
+            mine = getattr(self, name)
+            for k, v in sd[name].items():
+                if k not in mine or tuple(mine[k].shape) != tuple(v.shape):
+                    raise ValueError(f"Adam.load_state_dict: {name}[{k!r}] does not match")
+                mine[k].copy_(v.to(mine[k].device, dtype=mine[k].dtype))
+        self.count = int(sd["count"])
+        self.state = step_state(self.state.device, self.count)
+
     def step(self, params: dict, grads: dict):
         """One update; launches only kernels (graph-capturable unless the
         clip norm is all-reduced over a process group)."""
@@ -497,6 +518,51 @@ class TreeOptimizer:
                                               self.Q, T, ptr(self.grads["ancestors"]), st))
             self.opt.step(self.params, self.grads)
         return self.loss
+
+    # ------------------------------------------------------------------
+    # checkpoint / resume (the C5 loop's params + Adam state)
+    # ------------------------------------------------------------------
+    def state_dict(self) -> dict:
+        """Host copies of everything a resumed loop needs: tree_params,
+        ancestor logits and the Adam state (count, mu, nu).  S, G and the
+        other buffers are recomputed from them."""
+        return {"params": {k: v.detach().cpu().clone() for k, v in self.params.items()},
+                "opt": self.opt.state_dict()}
+
+    def load_state_dict(self, sd: dict):
+        for k, v in sd["params"].items():
+            if k not in self.params or tuple(self.params[k].shape) != tuple(v.shape):
+                raise ValueError(f"TreeOptimizer.load_state_dict: params[{k!r}] does not match")
+            self.params[k].copy_(v.to(self.params[k].device, dtype=self.params[k].dtype))
+        self.opt.load_state_dict(sd["opt"])
+        self._s_temperature = None  # the next step recomputes the ancestor rows of S
+
+    def save_checkpoint(self, path):
+        """``np.savez`` of ``state_dict`` (flat keys, no pickled objects)."""
+        sd = self.state_dict()
+        flat = {"count": np.asarray(sd["opt"]["count"], dtype=np.int64)}
+        for k, v in sd["params"].items():
+            flat[f"params/{k}"] = v.numpy()
+        for name in ("mu", "nu"):
+            for k, v in sd["opt"][name].items():
+                flat[f"{name}/{k}"] = v.numpy()
+        np.savez(path, **flat)
+
+    def load_checkpoint(self, path):
+        """Resume from ``save_checkpoint`` output (``np.load`` without pickle)."""
+        torch = _torch()
+        with np.load(path, allow_pickle=False) as z:
+            sd = {"params": {}, "opt": {"count": int(z["count"]), "mu": {}, "nu": {}}}
+            for key in z.files:
+                if "/" not in key:
+                    continue
+                group, name = key.split("/", 1)
+                t = torch.from_numpy(np.array(z[key]))
+                if group == "params":
+                    sd["params"][name] = t
+                else:
+                    sd["opt"][group][name] = t
+        self.load_state_dict(sd)
 
     # ------------------------------------------------------------------
     # device loop (graph-capturable step)
