@@ -2,7 +2,8 @@
 vs the uniform engine run tree by tree.
 
 Q <= 4 runs the lane-per-site kernel, Q = 5 / 20 / 61 the state-parallel
-one (each 64-site item split over ceil(64 / sites-per-wave) waves).
+one (each 64-site item split over ceil(64 / sites-per-wave) waves), Q = 100
+the large-alphabet one (a 128-thread workgroup walks the item's 64 sites).
 
 Bars: hard path bit-exact (dp, per-tree / per-site scores, trex backtrack);
 per-tree scores and dp also bitwise equal to a uniform SankoffEngine on the
@@ -41,7 +42,7 @@ def _ref(chs, leaves, cost, tau, dts):
             for b, (c, lv) in enumerate(zip(chs, leaves))]
 
 
-@pytest.mark.parametrize("Q", [2, 3, 4, 5, 20, 61])
+@pytest.mark.parametrize("Q", [2, 3, 4, 5, 20, 61, 100])
 def test_ragged_hard_matches_oracle_and_uniform(device, Q):
     chs, leaves = _batch(Q, seed=Q, missing=0.05)
     plan = RaggedTreePlan(chs, [L for _, L in SIZES])
@@ -74,7 +75,7 @@ def test_ragged_hard_matches_oracle_and_uniform(device, Q):
                                    rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize("Q", [4, 20])
+@pytest.mark.parametrize("Q", [4, 20, 100])
 @pytest.mark.parametrize("tau", [0.3, 1.0])
 def test_ragged_softmin_fused_vs_oracle(device, tau, Q):
     chs, leaves = _batch(Q, seed=40)
@@ -98,7 +99,7 @@ def test_ragged_softmin_fused_vs_oracle(device, tau, Q):
     assert torch.equal(mg, mg2)
 
 
-@pytest.mark.parametrize("Q", [4, 20, 61])
+@pytest.mark.parametrize("Q", [4, 20, 61, 100])
 def test_ragged_backtrack_matches_reference(device, Q):
     chs, leaves = _batch(Q, seed=60)
     plan = RaggedTreePlan(chs, [L for _, L in SIZES])
@@ -147,8 +148,9 @@ def test_from_padded_strips_trex_padding(device):
     assert shapes == [(2 * nl - 1, L) for nl, L in trees]
 
 
-def test_ragged_rejects_q_above_64(device):
+def test_ragged_rejects_q_above_128(device):
     chs, _ = _batch(4, seed=1)
     plan = RaggedTreePlan(chs, [L for _, L in SIZES])
+    RaggedSankoffEngine(plan, 128, device)
     with pytest.raises(NotImplementedError):
-        RaggedSankoffEngine(plan, 65, device)
+        RaggedSankoffEngine(plan, 129, device)

@@ -1483,6 +1483,7 @@ extern "C" int trex_dp_to_trex_layout(const float* dp, const int8_t* leaves, int
 // ---------------------------------------------------------------------------
 extern "C" int64_t trex_ragged_workspace_bytes(int64_t items, int Q) {
   if (items <= 0 || Q <= 0) return 0;
+  if (Q > kWideMaxQ) return items * 8 * (1 + (int64_t)Q * Q) + 256;  // partials per item
   if (Q > 4) return wide_ragged_workspace_bytes(items, Q);  // partials per wave
   return items * 8 * (1 + (int64_t)Q * Q) + 256;
 }
@@ -1498,9 +1499,9 @@ extern "C" int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_
   if (B <= 0 || items <= 0 || items > 0x7FFFFFFF || max_nl < 2 || Q < 2)
     return set_error(TREX_E_ARG, "%s: bad shape B=%d items=%lld max_nl=%d Q=%d", fn, B,
                      (long long)items, max_nl, Q);
-  if (Q > kWideMaxQ)
-    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build", fn, Q,
-                     kWideMaxQ);
+  if (Q > kBigMaxQ)
+    return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build (int8 leaf "
+                     "codes / ancestral states)", fn, Q, kBigMaxQ);
   if (!plan || !leaves || !cost || !workspace || !dp)
     return set_error(TREX_E_ARG, "%s: null pointer argument", fn);
   if ((phase & 1) && !tree_score) return set_error(TREX_E_ARG, "%s: tree_score is required", fn);
@@ -1537,6 +1538,7 @@ extern "C" int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_
     c.d_cost = d_cost;
     c.workspace = workspace;
     c.stream = stream;
+    if (Q > kWideMaxQ) return bigq_ragged_run(fn, c, meta, meta + (size_t)B * kRaggedMeta, items);
     return wide_ragged_run(fn, c, meta, meta + (size_t)B * kRaggedMeta, items);
   }
   const size_t lds = lds_bytes(n_slots, max_nl, Q, 1);
@@ -1585,15 +1587,16 @@ extern "C" int trex_sankoff_ragged_backtrack(const int32_t* plan, int B, int64_t
   const char* fn = "trex_sankoff_ragged_backtrack";
   if (B <= 0 || items <= 0 || items > 0x7FFFFFFF || steps <= 0 || Q < 2)
     return set_error(TREX_E_ARG, "%s: bad arguments", fn);
-  if (Q > kWideMaxQ)
+  if (Q > kBigMaxQ)
     return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d not supported by this build", fn, Q,
-                     kWideMaxQ);
+                     kBigMaxQ);
   if (!backtrack_ok)
     return set_error(TREX_E_TOPOLOGY,
                      "%s: the reference backtrack does not terminate on this batch (cyclic child "
                      "references)", fn);
   if (!plan || !cost || !dp || !anc_states) return set_error(TREX_E_ARG, "%s: null pointer", fn);
   const int* meta = plan + TREX_PLAN_HEADER_INTS;
+  if (Q > kWideMaxQ) return bigq_ragged_backtrack(meta, B, items, steps, cost, dp, Q, anc_states, stream);
   if (Q > 4) return wide_ragged_backtrack(meta, B, items, steps, cost, dp, Q, anc_states, stream);
   hipStream_t st = (hipStream_t)stream;
 #define TREX_RBT(QQ)                                                                          \

@@ -37,6 +37,7 @@ namespace trex {
 namespace {
 
 constexpr int kBigT = 16;         // sites per workgroup (walked in turn)
+constexpr int kBigRaggedT = 64;   // ragged batches: the plan's (tree, 64-site) items
 constexpr int kBigThreads = 128;  // = the largest alphabet: thread i = state i
 
 struct BigArgs {
@@ -51,8 +52,12 @@ struct BigArgs {
   const float* dts;   // [B] or null
   float* marg;        // [B][n_int][L][Q] or null
   int8_t* anc;        // [B][n_int][L] or null
-  double* part_tree;  // [B * tiles]
-  double* part_dc;    // [Q * Q][B * tiles]
+  double* part_tree;  // [B * tiles] (ragged: [items])
+  double* part_dc;    // [Q * Q][B * tiles] (ragged: [Q * Q][items])
+  // ragged batches (trex_ragged_plan_build): per-tree records, item -> tree
+  const int* rmeta;
+  const int* ritem;
+  int nitems;
 };
 
 // block-wide reductions over the 128 threads (two waves): min, sum, and the
@@ -90,7 +95,7 @@ __device__ __forceinline__ int block_argmax_first(float v, bool own, float* red)
   return bi;
 }
 
-template <int PHASE, bool SOFT>
+template <int PHASE, bool SOFT, bool RAGGED>
 __global__ __launch_bounds__(kBigThreads) void sankoff_bigq_kernel(BigArgs A) {
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
@@ -98,10 +103,31 @@ __global__ __launch_bounds__(kBigThreads) void sankoff_bigq_kernel(BigArgs A) {
   const int Q = A.Q, QP = Q + 1;
   const int i = threadIdx.x;  // parent state (forward) / child state (column sums)
   const bool own = i < Q;
-  const int ni = A.n_int, L = A.L, nl = A.nl;
-  const int tree = blockIdx.x / A.tiles;
-  const int tile = blockIdx.x - tree * A.tiles;
-  const int nb = A.B * A.tiles;
+  int ni, L, tree, tile;
+  size_t leaf_base, rows_base, site_base;
+  const int4* prog;
+  if constexpr (RAGGED) {  // one (tree, 64-site) item of the ragged plan
+    tree = A.ritem[blockIdx.x];
+    const int* m = A.rmeta + (size_t)tree * kRaggedMeta;
+    ni = m[1];
+    L = m[3];
+    site_base = (size_t)(uint32_t)m[4];
+    tile = blockIdx.x - m[5];
+    leaf_base = (size_t)(uint32_t)m[6] | ((size_t)(uint32_t)m[7] << 32);
+    rows_base = (size_t)(uint32_t)m[8] | ((size_t)(uint32_t)m[9] << 32);
+    prog = A.steps + m[0];
+  } else {
+    ni = A.n_int;
+    L = A.L;
+    tree = blockIdx.x / A.tiles;
+    tile = blockIdx.x - tree * A.tiles;
+    site_base = (size_t)tree * L;
+    leaf_base = (size_t)tree * A.nl * L;
+    rows_base = (size_t)tree * ni * L;
+    prog = A.steps + (size_t)tree * ni;
+  }
+  constexpr int TS = RAGGED ? kBigRaggedT : kBigT;  // sites walked by this workgroup
+  const int nb = RAGGED ? A.nitems : A.B * A.tiles;
   const float a = A.a, bcoef = A.bcoef;
 
   // ---- LDS: C [Q][Q+1] | dC [Q][Q+1] | slots [n_slots+1][Q] | prev [2][Q] |
@@ -122,9 +148,8 @@ __global__ __launch_bounds__(kBigThreads) void sankoff_bigq_kernel(BigArgs A) {
   }
   __syncthreads();
 
-  const int4* prog = A.steps + (size_t)tree * ni;
-  const int8_t* lv = A.leaves + (size_t)tree * nl * L;
-  float* dpt = A.dp + (size_t)tree * ni * L * Q;
+  const int8_t* lv = A.leaves + leaf_base;
+  float* dpt = A.dp + rows_base * Q;
   const float fts = A.dts ? A.dts[tree] : 1.0f;
   double tree_part = 0.0;
 
@@ -150,8 +175,8 @@ __global__ __launch_bounds__(kBigThreads) void sankoff_bigq_kernel(BigArgs A) {
     return ((unsigned)c < (unsigned)Q) ? c : Q;
   };
 
-  for (int s = 0; s < kBigT; ++s) {
-    const int site = tile * kBigT + s;
+  for (int s = 0; s < TS; ++s) {
+    const int site = tile * TS + s;
     if (site >= L) break;  // uniform
     float* drow = dpt + (size_t)site * Q;  // + row * L * Q
     float dv = 0.0f;
@@ -198,7 +223,7 @@ __global__ __launch_bounds__(kBigThreads) void sankoff_bigq_kernel(BigArgs A) {
     }
     if constexpr (FWD) {
       if (i == 0) {
-        if (A.site_score) A.site_score[(size_t)tree * L + site] = score;
+        if (A.site_score) A.site_score[site_base + site] = score;
         tree_part += (double)score;
       }
     }
@@ -214,10 +239,10 @@ __global__ __launch_bounds__(kBigThreads) void sankoff_bigq_kernel(BigArgs A) {
                                                      : slots[((stp.w & kStepRoot) ? A.n_slots
                                                                                   : ((stp.x >> 16) & 0xFF)) * Q + i])
                             : 0.0f;
-        if (A.marg && own) A.marg[((size_t)tree * ni + row) * L * Q + (size_t)site * Q + i] = g;
+        if (A.marg && own) A.marg[(rows_base + (size_t)row * L + site) * Q + i] = g;
         if (A.anc) {
           const int bi = block_argmax_first(g, own, red);
-          if (i == 0) A.anc[((size_t)tree * ni + row) * L + site] = (int8_t)bi;
+          if (i == 0) A.anc[rows_base + (size_t)row * L + site] = (int8_t)bi;
         }
         __syncthreads();  // g read from its slot before children overwrite slots
         for (int c = 0; c < 2; ++c) {
@@ -293,18 +318,35 @@ __global__ __launch_bounds__(kBigThreads) void sankoff_bigq_kernel(BigArgs A) {
 // lane per site walks the host-simulated DFS order (plan.cpp), C in LDS,
 // each step's DP row streamed from the table, trex's strict-< scan (the
 // first argmin); parent states of visited nodes in LDS.
+// Ragged batches (no bound on a tree's node count at launch) re-read the
+// parent's state from this lane's own output instead of the LDS array.
+template <bool RAGGED>
 __global__ __launch_bounds__(kWave) void bigq_backtrack_kernel(const int* __restrict__ bt,
                                                                 const float* __restrict__ cost,
                                                                 const float* __restrict__ dp,
                                                                 int n_int, int L, int Q, int tiles,
-                                                                int8_t* __restrict__ anc) {
+                                                                int8_t* __restrict__ anc,
+                                                                const int* __restrict__ rmeta,
+                                                                int B, int items, int steps) {
   extern __shared__ __attribute__((aligned(16))) float bl[];
   float* c = bl;                                          // [Q][Q]
   int8_t* sts = reinterpret_cast<int8_t*>(bl + Q * Q);    // [n_int][64]
-  const int tree = blockIdx.x / tiles;
-  const int tile = blockIdx.x - tree * tiles;
-  const size_t rows_base = (size_t)tree * n_int * L;
-  bt += (size_t)tree * n_int * 2;
+  int tree, tile;
+  size_t rows_base;
+  if constexpr (RAGGED) {
+    tree = rmeta[(size_t)B * kRaggedMeta + blockIdx.x];
+    const int* m = rmeta + (size_t)tree * kRaggedMeta;
+    n_int = m[1];
+    L = m[3];
+    tile = blockIdx.x - m[5];
+    rows_base = (size_t)(uint32_t)m[8] | ((size_t)(uint32_t)m[9] << 32);
+    bt = rmeta + (size_t)B * kRaggedMeta + items + (size_t)steps * 4 + (size_t)m[0] * 2;
+  } else {
+    tree = blockIdx.x / tiles;
+    tile = blockIdx.x - tree * tiles;
+    rows_base = (size_t)tree * n_int * L;
+    bt += (size_t)tree * n_int * 2;
+  }
   const int lane = threadIdx.x;
   for (int t = lane; t < Q * Q; t += kWave) c[t] = cost[t];
   __syncthreads();
@@ -327,7 +369,8 @@ __global__ __launch_bounds__(kWave) void bigq_backtrack_kernel(const int* __rest
           if (v < bv) { bv = v; out = j; }
         }
       } else {
-        const float* row = c + (int)sts[ey * kWave + lane] * Q;
+        const int sp = RAGGED ? (int)at[(size_t)ey * L] : (int)sts[ey * kWave + lane];
+        const float* row = c + sp * Q;
         float bv = row[0] + (sent ? kSentinel : d[0]);
         for (int j = 1; j < Q; ++j) {
           const float v = row[j] + (sent ? kSentinel : d[j]);
@@ -335,7 +378,7 @@ __global__ __launch_bounds__(kWave) void bigq_backtrack_kernel(const int* __rest
         }
       }
     }
-    sts[x * kWave + lane] = (int8_t)out;
+    if constexpr (!RAGGED) sts[x * kWave + lane] = (int8_t)out;
     at[(size_t)x * L] = (int8_t)out;
   }
 }
@@ -350,6 +393,28 @@ int64_t bigq_workspace_bytes(int B, int L, int Q) {
 
 size_t bigq_lds_bytes(int n_slots, int Q) {
   return ((size_t)2 * Q * (Q + 1) + (size_t)(n_slots + 1) * Q + 6 * (size_t)Q + kBigThreads) * 4;
+}
+
+template <bool RAGGED>
+int bigq_launch(const char* fn, const BigArgs& A, const WideCall& c, int64_t nb, size_t lds) {
+  hipStream_t st = (hipStream_t)c.stream;
+  auto go = [&](auto kernel) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)nb), dim3(kBigThreads), lds, st, A);
+  };
+  if (c.soft) {
+    if (c.phase == 1) go(sankoff_bigq_kernel<1, true, RAGGED>);
+    else if (c.phase == 2) go(sankoff_bigq_kernel<2, true, RAGGED>);
+    else go(sankoff_bigq_kernel<3, true, RAGGED>);
+  } else {
+    if (c.phase == 1) go(sankoff_bigq_kernel<1, false, RAGGED>);
+    else if (c.phase == 2) go(sankoff_bigq_kernel<2, false, RAGGED>);
+    else go(sankoff_bigq_kernel<3, false, RAGGED>);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  return TREX_OK;
 }
 
 int bigq_run(const char* fn, const WideCall& c) {
@@ -380,25 +445,48 @@ int bigq_run(const char* fn, const WideCall& c) {
   const int64_t nb = (int64_t)c.B * tiles;
   A.part_tree = static_cast<double*>(c.workspace);
   A.part_dc = A.part_tree + nb;
-  hipStream_t st = (hipStream_t)c.stream;
-  auto go = [&](auto kernel) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kernel, dim3((unsigned)nb), dim3(kBigThreads), lds, st, A);
-  };
-  if (c.soft) {
-    if (c.phase == 1) go(sankoff_bigq_kernel<1, true>);
-    else if (c.phase == 2) go(sankoff_bigq_kernel<2, true>);
-    else go(sankoff_bigq_kernel<3, true>);
-  } else {
-    if (c.phase == 1) go(sankoff_bigq_kernel<1, false>);
-    else if (c.phase == 2) go(sankoff_bigq_kernel<2, false>);
-    else go(sankoff_bigq_kernel<3, false>);
-  }
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
+  A.rmeta = nullptr;
+  A.ritem = nullptr;
+  A.nitems = 0;
+  if (int e = bigq_launch<false>(fn, A, c, (int64_t)nb, lds)) return e;
   return partial_reduce(fn, A.part_tree, A.part_dc, c.B, tiles, c.Q, c.phase, c.tree_score,
                         c.d_cost, c.stream);
+}
+
+// ragged batches: the plan's (tree, 64-site) items, per-item partials summed
+// per tree by the ragged partial reduce
+int bigq_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const int* ritem,
+                    int64_t items) {
+  const size_t lds = bigq_lds_bytes(c.n_slots, c.Q);
+  if (c.Q > kBigMaxQ) return set_error(TREX_E_UNSUPPORTED, "%s: Q=%d > %d", fn, c.Q, kBigMaxQ);
+  if (lds > 160 * 1024) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
+  BigArgs A;
+  A.steps = reinterpret_cast<const int4*>(c.steps);
+  A.leaves = c.leaves;
+  A.cost = c.cost;
+  A.n_int = 0;
+  A.nl = c.nl;
+  A.L = 0;
+  A.tiles = 0;
+  A.B = c.B;
+  A.Q = c.Q;
+  A.n_slots = c.n_slots;
+  A.a = c.a;
+  A.bcoef = c.bcoef;
+  A.hard_root = c.hard_root;
+  A.dp = c.dp;
+  A.site_score = c.site_score;
+  A.dts = c.dts;
+  A.marg = c.marg;
+  A.anc = c.anc;
+  A.part_tree = static_cast<double*>(c.workspace);
+  A.part_dc = A.part_tree + items;
+  A.rmeta = rmeta;
+  A.ritem = ritem;
+  A.nitems = (int)items;
+  if (int e = bigq_launch<true>(fn, A, c, items, lds)) return e;
+  return partial_reduce(fn, A.part_tree, A.part_dc, c.B, 0, c.Q, c.phase, c.tree_score, c.d_cost,
+                        c.stream, rmeta + 5, kRaggedMeta, (int)items);
 }
 
 int bigq_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
@@ -407,12 +495,26 @@ int bigq_backtrack(const int32_t* bt, const float* cost, const float* dp, int B,
   const size_t lds = (size_t)Q * Q * 4 + (size_t)ni * kWave;
   if (lds > 160 * 1024)
     return set_error(TREX_E_UNSUPPORTED, "trex_sankoff_backtrack: %d internal nodes at Q=%d", ni, Q);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bigq_backtrack_kernel),
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bigq_backtrack_kernel<false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(bigq_backtrack_kernel, dim3((unsigned)((int64_t)B * tiles)), dim3(kWave), lds,
-                     (hipStream_t)stream, bt, cost, dp, ni, L, Q, tiles, anc);
+  hipLaunchKernelGGL(bigq_backtrack_kernel<false>, dim3((unsigned)((int64_t)B * tiles)), dim3(kWave),
+                     lds, (hipStream_t)stream, bt, cost, dp, ni, L, Q, tiles, anc, nullptr, 0, 0, 0);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "trex_sankoff_backtrack: %s", hipGetErrorString(e));
+  return TREX_OK;
+}
+
+int bigq_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,
+                          const float* cost, const float* dp, int Q, int8_t* anc, void* stream) {
+  const size_t lds = (size_t)Q * Q * 4;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(bigq_backtrack_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(bigq_backtrack_kernel<true>, dim3((unsigned)items), dim3(kWave), lds,
+                     (hipStream_t)stream, nullptr, cost, dp, 0, 0, Q, 0, anc, rmeta, B, (int)items,
+                     (int)steps);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return set_error(TREX_E_HIP, "trex_sankoff_ragged_backtrack: %s", hipGetErrorString(e));
   return TREX_OK;
 }
 

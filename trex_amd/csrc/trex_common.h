@@ -116,6 +116,10 @@ int64_t bigq_workspace_bytes(int B, int L, int Q);
 int bigq_run(const char* fn, const WideCall& c);
 int bigq_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream);
+int bigq_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const int* ritem,
+                    int64_t items);
+int bigq_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,
+                          const float* cost, const float* dp, int Q, int8_t* anc, void* stream);
 constexpr int kRaggedMeta = 12;  // ints per tree record of a ragged plan (plan.cpp)  // leaf codes and ancestral states are int8
 int wide_group(int Q);
 int wide_tiles(int L, int Q);

@@ -104,8 +104,9 @@ class RaggedTreePlan:
 
 
 class RaggedSankoffEngine:
-    """Sankoff over a ragged batch on the device (Q <= 64: Q <= 4 lane per
-    site, larger alphabets state-parallel, sankoff_wide.hip).
+    """Sankoff over a ragged batch on the device (Q <= 128: Q <= 4 lane per
+    site, up to 64 states state-parallel (sankoff_wide.hip), 64 < Q <= 128 a
+    workgroup per state vector (sankoff_bigq.hip)).
 
     leaves: packed int8 device tensor (RaggedTreePlan.pack_leaves); cost (Q, Q)
     float32.  Mirrors SankoffEngine's forward / backward / fwd_bwd /
@@ -114,8 +115,9 @@ class RaggedSankoffEngine:
 
     def __init__(self, plan: RaggedTreePlan, n_states: int, device=None):
         torch = _torch()
-        if n_states > 64:
-            raise NotImplementedError("alphabets above 64 states are not supported")
+        if n_states > 128:
+            raise NotImplementedError("alphabets above 128 states are not supported "
+                                      "(int8 leaf codes / ancestral states)")
         self.plan = plan
         self.Q = int(n_states)
         self.device = torch.device(device) if device is not None else torch.device(
