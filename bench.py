@@ -596,7 +596,6 @@ def nk_line(torch, device, steps=50, warmup=5):
     binary states, K = 10, lambda = 3) and at a larger DNA shape."""
     from trex_amd import nk as NK
     from trex_amd.datagen import create_nk_model_landscape
-    from trex_amd.tree import Adam
 
     out = {}
     for name, (nl, L, Q, k, lam) in {"eval_32x15_q2_k10": (32, 15, 2, 10, 3.0),
@@ -610,15 +609,13 @@ def nk_line(torch, device, steps=50, warmup=5):
         land = NK.NKLandscape(inter, F, Q, device)
         S0 = NK.masked_sequences_from_leaves(rng.integers(0, Q, size=(nl, L)), n_all, Q, device)
         fn = NK.LandscapeAwareLoss(A, nl, land, lam, k)
-        params = {"ancestors": torch.as_tensor(rng.normal(size=(nl - 1, L, Q)), dtype=torch.float32,
-                                               device=device)}
-        opt = Adam(params, 1e-3)
-
-        gbuf = torch.empty_like(params["ancestors"])
+        # run_trex_landscape_aware_configurable's Adam step: loss + dS, then
+        # the update_seq VJP, Adam and the next update_seq in one pass
+        opt = NK.LandscapeAwareAdam(fn, rng.normal(size=(nl - 1, L, Q)).astype(np.float32), S0,
+                                    1e-3)
 
         def step():
-            _, g = fn.value_and_grad(params["ancestors"], S0, out=gbuf)
-            opt.step(params, {"ancestors": g})
+            opt.step()
 
         for _ in range(warmup):
             step()

@@ -221,3 +221,40 @@ def test_nk_adam_step_graph_replay_is_bitwise_eager(device):
         runs.append((float(fn.loss[0]), params["ancestors"].clone()))
     assert runs[1][0] == runs[0][0] and torch.equal(runs[1][1], runs[0][1])
     assert runs[2][0] == runs[0][0] and torch.equal(runs[2][1], runs[0][1])
+
+
+@pytest.mark.parametrize("capture", [False, True])
+def test_nk_fused_adam_is_bitwise_the_unfused_loop(device, capture):
+    """LandscapeAwareAdam (update_seq VJP + Adam + next update_seq in one
+    pass, trex_adam_seq_update_step_dev) == value_and_grad + Adam.step,
+    bitwise, over 6 steps at the eval shape -- eager and as hipGraph replays
+    of one captured step."""
+    from trex_amd.tree import Adam
+
+    c = _case(32, 15, 2, 10, seed=7)
+    land = NK.NKLandscape(c["inter"], c["F"], 2, device)
+    S0 = torch.as_tensor(c["S0"], device=device)
+    fn = NK.LandscapeAwareLoss(c["A"], c["n_leaves"], land, 3.0, 10)
+    params = {"ancestors": torch.as_tensor(c["anc"], device=device).clone()}
+    opt = Adam(params, 1e-3)
+    ref_losses = []
+    for _ in range(6):
+        loss, g = fn.value_and_grad(params["ancestors"], S0)
+        ref_losses.append(float(loss[0]))
+        opt.step(params, {"ancestors": g})
+    fn2 = NK.LandscapeAwareLoss(c["A"], c["n_leaves"], land, 3.0, 10)
+    fused = NK.LandscapeAwareAdam(fn2, c["anc"], S0, 1e-3)
+    losses = []
+    if capture:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fused.step()
+        for _ in range(6):
+            graph.replay()
+            losses.append(float(fn2.loss[0]))
+    else:
+        for _ in range(6):
+            losses.append(float(fused.step()[0]))
+    assert losses == ref_losses
+    assert torch.equal(fused.ancestors, params["ancestors"])
+    assert torch.equal(fused.mu, opt.mu["ancestors"]) and torch.equal(fused.nu, opt.nu["ancestors"])

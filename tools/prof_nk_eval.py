@@ -16,7 +16,6 @@ if __name__ == "__main__":
 
     from trex_amd import nk as NK
     from trex_amd.datagen import create_nk_model_landscape
-    from trex_amd.tree import Adam
 
     dev = torch.device("cuda", 0)
     nl, L, Q, k, lam = 32, 15, 2, 10, 3.0
@@ -28,14 +27,10 @@ if __name__ == "__main__":
     land = NK.NKLandscape(land_np["interactions"], land_np["fitness_tables"], Q, dev)
     S0 = NK.masked_sequences_from_leaves(rng.integers(0, Q, size=(nl, L)), n_all, Q, dev)
     fn = NK.LandscapeAwareLoss(A, nl, land, lam, k)
-    params = {"ancestors": torch.as_tensor(rng.normal(size=(nl - 1, L, Q)), dtype=torch.float32,
-                                           device=dev)}
-    opt = Adam(params, 1e-3)
-    gbuf = torch.empty_like(params["ancestors"])
+    opt = NK.LandscapeAwareAdam(fn, rng.normal(size=(nl - 1, L, Q)).astype(np.float32), S0, 1e-3)
 
     def step():
-        fn.value_and_grad(params["ancestors"], S0, out=gbuf)
-        opt.step(params, {"ancestors": gbuf})
+        opt.step()
 
     for _ in range(5):
         step()

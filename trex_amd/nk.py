@@ -24,7 +24,6 @@ from __future__ import annotations
 import numpy as np
 
 from ._lib import check, lib, ptr, stream_handle
-from .tree import Adam
 
 
 def _torch():
@@ -165,17 +164,32 @@ class LandscapeAwareLoss:
         n_anc = self.N - self.n_leaves
         if tuple(anc.shape) != (n_anc, self.L, self.Q):
             raise ValueError(f"ancestors must be {(n_anc, self.L, self.Q)}")
-        # S = masked_sequences with the ancestor rows rewritten below: the
-        # copy is needed only when the caller passes another tensor or wrote
-        # into this one (torch's version counter); the cached reference keeps
-        # the tensor alive, so its storage cannot be reused under the cache
-        ms = _f32(masked_sequences, dev)
+        self._set_leaves(masked_sequences)
+        check(L_.trex_tree_update_seq(ptr(anc), n_anc, self.L, self.Q, self.T,
+                                      ptr(self.S[self.n_leaves:]), st))
+        dS = self._loss_and_dS(want_grad)
+        if not want_grad:
+            return self.loss, None
+        d_anc = torch.empty_like(anc) if out is None else out
+        check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaves:]), ptr(dS[self.n_leaves:]),
+                                          n_anc, self.L, self.Q, self.T, ptr(d_anc), st))
+        return self.loss, d_anc
+
+    def _set_leaves(self, masked_sequences):
+        # S = masked_sequences with the ancestor rows rewritten: the copy is
+        # needed only when the caller passes another tensor or wrote into
+        # this one (torch's version counter); the cached reference keeps the
+        # tensor alive, so its storage cannot be reused under the cache
+        ms = _f32(masked_sequences, self.S.device)
         ver = getattr(ms, "_version", None)
         if ms is not self._s_src or ver is None or ver != self._s_ver:
             self.S.copy_(ms)
             self._s_src, self._s_ver = ms, ver
-        check(L_.trex_tree_update_seq(ptr(anc), n_anc, self.L, self.Q, self.T,
-                                      ptr(self.S[self.n_leaves:]), st))
+
+    def _loss_and_dS(self, want_grad: bool):
+        """Loss and d loss / d S (all rows) of the current S."""
+        L_ = lib()
+        st = stream_handle(self.S.device)
         K = self.L * self.Q
         check(L_.trex_tree_surrogate(ptr(self.S), ptr(self.A), self.N, K, ptr(self.sur),
                                      ptr(self.dS_sur) if want_grad else None,
@@ -188,16 +202,59 @@ class LandscapeAwareLoss:
                 ptr(self.mask), self.n_valid, self.lam, self.n_nonroot, ptr(self.sur),
                 ptr(self.dS_sur) if want_grad else None, ptr(self.loss),
                 ptr(self.dS) if want_grad else None, ptr(self.nk_ws), self.nk_ws.numel(), st))
-            dS = self.dS
-        else:
-            self.loss.copy_(self.sur)
-            dS = self.dS_sur
-        if not want_grad:
-            return self.loss, None
-        d_anc = torch.empty_like(anc) if out is None else out
-        check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaves:]), ptr(dS[self.n_leaves:]),
-                                          n_anc, self.L, self.Q, self.T, ptr(d_anc), st))
-        return self.loss, d_anc
+            return self.dS
+        self.loss.copy_(self.sur)
+        return self.dS_sur
+
+
+class LandscapeAwareAdam:
+    """optax.adam on the ancestor logits of a LandscapeAwareLoss, one fused
+    step: the loss and dS of the current S, then the update_seq VJP, the Adam
+    update and the next step's update_seq in one pass over the logits
+    (trex_adam_seq_update_step_dev) -- bitwise the loop
+    ``loss, g = fn.value_and_grad(anc, S0); Adam.step(...)`` of
+    run_trex_landscape_aware_configurable (benchmark.py:326-460), two
+    launches fewer per step.  The step count lives on the device, so a
+    captured step replays (``step()`` launches only kernels)."""
+
+    def __init__(self, fn: LandscapeAwareLoss, ancestors, masked_sequences, lr: float = 1e-3,
+                 b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8):
+        torch = _torch()
+        from .tree import step_state
+
+        self.fn = fn
+        dev = fn.S.device
+        self.ancestors = _f32(ancestors, dev).clone()
+        n_anc = fn.N - fn.n_leaves
+        if tuple(self.ancestors.shape) != (n_anc, fn.L, fn.Q):
+            raise ValueError(f"ancestors must be {(n_anc, fn.L, fn.Q)}")
+        self.lr, self.b1, self.b2, self.eps = float(lr), float(b1), float(b2), float(eps)
+        self.mu = torch.zeros_like(self.ancestors)
+        self.nu = torch.zeros_like(self.ancestors)
+        self.count = 0
+        # device step record: count / bias corrections advance per step, the
+        # update_seq temperature (fixed for this loss) in T and T_next
+        self.state = step_state(dev)
+        tbits = int(np.array([fn.T], dtype=np.float32).view(np.int32)[0])
+        self.state[3] = tbits
+        self.state[4] = tbits
+        fn._set_leaves(masked_sequences)
+        check(lib().trex_tree_update_seq(ptr(self.ancestors), n_anc, fn.L, fn.Q, fn.T,
+                                         ptr(fn.S[fn.n_leaves:]), stream_handle(dev)))
+
+    def step(self):
+        """One step; returns the (device) loss before the update."""
+        fn = self.fn
+        L_ = lib()
+        st = stream_handle(fn.S.device)
+        dS = fn._loss_and_dS(True)
+        self.count += 1
+        check(L_.trex_step_advance(ptr(self.state), self.b1, self.b2, None, 0, st))
+        check(L_.trex_adam_seq_update_step_dev(ptr(dS[fn.n_leaves:]), fn.N - fn.n_leaves, fn.L,
+                                               fn.Q, ptr(self.state), ptr(self.ancestors),
+                                               ptr(self.mu), ptr(self.nu), self.lr, self.b1,
+                                               self.b2, self.eps, ptr(fn.S[fn.n_leaves:]), st))
+        return fn.loss
 
 
 def landscape_aware_loss(ancestors, masked_sequences, n_leaves: int, landscape: NKLandscape,
@@ -237,14 +294,12 @@ def run_trex_landscape_aware_configurable(leaf_sequences, n_all: int, n_leaves: 
     S0 = masked_sequences_from_leaves(leaf_sequences, n_all, n_states, dev)
     fn = LandscapeAwareLoss(adj_matrix, n_leaves, landscape, lambda_val, real_k,
                             seq_mask=seq_mask)
-    params = {"ancestors": _f32(init_ancestors, dev).clone()}
-    opt = Adam(params, learning_rate)
+    opt = LandscapeAwareAdam(fn, init_ancestors, S0, learning_rate)
     losses = torch.empty((n_iterations,), dtype=torch.float32, device=dev) if return_losses \
         else None
     for it in range(n_iterations):
-        loss, g = fn.value_and_grad(params["ancestors"], S0)
+        loss = opt.step()
         if losses is not None:
             losses[it:it + 1].copy_(loss)
-        opt.step(params, {"ancestors": g})
-    out = torch.argmax(params["ancestors"], dim=-1)
+    out = torch.argmax(opt.ancestors, dim=-1)
     return (out, losses) if return_losses else out
