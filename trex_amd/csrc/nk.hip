@@ -278,6 +278,62 @@ __global__ __launch_bounds__(512) void nk_logits_bwd_kernel(NkArgs a, const floa
 // the slices' partial sums combine in fixed slice order.  Same products
 // (left to right over the neighbours, the reference's successive outer
 // products) and prefix / suffix gradients as the kernels above.
+// masked cross-entropy of every child of parent pc at site l against
+// log_softmax of the parent's logits xv (benchmark.py:288-302): d logits,
+// d child rows, the (pc, l) partial of the loss
+struct NkCe {
+  const float* S;
+  const int32_t* cofs;
+  const int32_t* cidx;
+  const float* mask;
+  float scale;
+  float* dlog;
+  float* dchild;
+  double* part;
+};
+__device__ __forceinline__ void nk_ce_one(const NkCe& c, const float (&xv)[kNkMaxQ], int pc, int l,
+                                          int L, int Q) {
+  const size_t t = (size_t)pc * L + l;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < kNkMaxQ; ++s) mx = fmaxf(mx, xv[s]);
+  float se = 0.0f;
+#pragma unroll
+  for (int s = 0; s < kNkMaxQ; ++s)
+    if (s < Q) se += expf(xv[s] - mx);
+  const float lse = mx + logf(se);
+  const float mk = c.mask ? c.mask[l] : 1.0f;
+  float dl[kNkMaxQ];
+#pragma unroll
+  for (int s = 0; s < kNkMaxQ; ++s) dl[s] = 0.0f;
+  double ce = 0.0;
+  for (int e = c.cofs[pc]; e < c.cofs[pc + 1]; ++e) {
+    const int n = c.cidx[e];
+    const float* sn = c.S + ((size_t)n * L + l) * Q;
+    float* dc = c.dchild + ((size_t)n * L + l) * Q;
+    float tot = 0.0f, cen = 0.0f;
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s)
+      if (s < Q) {
+        const float v = sn[s];
+        const float lp = xv[s] - lse;
+        tot += v;
+        cen -= v * lp;
+        dc[s] = -c.scale * mk * lp;
+        dl[s] -= v;
+      }
+#pragma unroll
+    for (int s = 0; s < kNkMaxQ; ++s)
+      if (s < Q) dl[s] += expf(xv[s] - lse) * tot;
+    ce += (double)(mk * cen);
+  }
+  float* dlo = c.dlog + t * Q;
+#pragma unroll
+  for (int s = 0; s < kNkMaxQ; ++s)
+    if (s < Q) dlo[s] = c.scale * mk * dl[s];
+  c.part[t] = ce;
+}
+
 constexpr int kNkSmallThreads = 256;
 constexpr int kNkSlices = 8;
 constexpr int kNkSmallP = kNkSmallThreads / kNkSlices;  // parents per block
@@ -325,9 +381,12 @@ __device__ __forceinline__ void small_stage(const NkArgs& a, int site, int p0, f
   }
 }
 
-template <int QT>
+// CE: the parent's logits go straight into the cross-entropy of its
+// children (nk_ce_one, the nk_ce_kernel arithmetic) instead of to HBM
+template <int QT, bool CE>
 __global__ __launch_bounds__(kNkSmallThreads) void nk_logits_small_kernel(NkArgs a,
-                                                                         float* __restrict__ logits) {
+                                                                         float* __restrict__ logits,
+                                                                         NkCe ce) {
   constexpr int MQ = QT ? QT : kNkMaxQ;
   const int Q = QT ? QT : a.Q;
   const int k = a.k;
@@ -347,7 +406,7 @@ __global__ __launch_bounds__(kNkSmallThreads) void nk_logits_small_kernel(NkArgs
   int d[kNkMaxK];
   small_digits(w.lo, k, Q, d);
   for (int idx = w.lo; idx < w.hi; ++idx) {
-    float prod = P[d[0]];
+    float prod = k > 0 ? P[d[0]] : 1.0f;  // k = 0: the table alone (one joint state)
 #pragma unroll
     for (int j = 1; j < kNkMaxK; ++j)
       if (j < k) prod = prod * P[j * Q + d[j]];
@@ -362,11 +421,18 @@ __global__ __launch_bounds__(kNkSmallThreads) void nk_logits_small_kernel(NkArgs
   __syncthreads();
   const int r = p0 + pp;
   if (sl != 0 || r >= a.R) return;
+  float xv[kNkMaxQ];
+#pragma unroll
+  for (int s = 0; s < kNkMaxQ; ++s) xv[s] = -INFINITY;
   for (int s = 0; s < Q; ++s) {
     float v = red[(size_t)pp * Q + s];
     for (int y = 1; y < kNkSlices; ++y) v += red[((size_t)y * kNkSmallP + pp) * Q + s];
-    logits[((size_t)r * a.L + site) * Q + s] = v;
+    if constexpr (CE)
+      xv[s] = v;
+    else
+      logits[((size_t)r * a.L + site) * Q + s] = v;
   }
+  if constexpr (CE) nk_ce_one(ce, xv, r, site, a.L, Q);
 }
 
 template <int QT>
@@ -454,54 +520,15 @@ __global__ __launch_bounds__(256) void nk_ce_kernel(const float* __restrict__ S,
                                                     int Q, float scale, float* __restrict__ dlog,
                                                     float* __restrict__ dchild,
                                                     double* __restrict__ part) {
+  const NkCe ce{S, cofs, cidx, mask, scale, dlog, dchild, part};
   const int64_t total = (int64_t)nP * L;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int l = (int)(t % L);
-    const int pc = (int)(t / L);
     const float* x = logits + (size_t)t * Q;
     float xv[kNkMaxQ];
-    float mx = -INFINITY;
 #pragma unroll
-    for (int s = 0; s < kNkMaxQ; ++s) {
-      xv[s] = s < Q ? x[s] : -INFINITY;
-      mx = fmaxf(mx, xv[s]);
-    }
-    float se = 0.0f;
-#pragma unroll
-    for (int s = 0; s < kNkMaxQ; ++s)
-      if (s < Q) se += expf(xv[s] - mx);
-    const float lse = mx + logf(se);
-    const float mk = mask ? mask[l] : 1.0f;
-    float dl[kNkMaxQ];
-#pragma unroll
-    for (int s = 0; s < kNkMaxQ; ++s) dl[s] = 0.0f;
-    double ce = 0.0;
-    for (int e = cofs[pc]; e < cofs[pc + 1]; ++e) {
-      const int n = cidx[e];
-      const float* sn = S + ((size_t)n * L + l) * Q;
-      float* dc = dchild + ((size_t)n * L + l) * Q;
-      float tot = 0.0f, cen = 0.0f;
-#pragma unroll
-      for (int s = 0; s < kNkMaxQ; ++s)
-        if (s < Q) {
-          const float v = sn[s];
-          const float lp = xv[s] - lse;
-          tot += v;
-          cen -= v * lp;
-          dc[s] = -scale * mk * lp;
-          dl[s] -= v;
-        }
-#pragma unroll
-      for (int s = 0; s < kNkMaxQ; ++s)
-        if (s < Q) dl[s] += expf(xv[s] - lse) * tot;
-      ce += (double)(mk * cen);
-    }
-    float* dlo = dlog + (size_t)t * Q;
-#pragma unroll
-    for (int s = 0; s < kNkMaxQ; ++s)
-      if (s < Q) dlo[s] = scale * mk * dl[s];
-    part[t] = ce;
+    for (int s = 0; s < kNkMaxQ; ++s) xv[s] = s < Q ? x[s] : -INFINITY;
+    nk_ce_one(ce, xv, (int)(t / L), (int)(t % L), L, Q);
   }
 }
 
@@ -608,16 +635,31 @@ int nk_slices(int R, int L, int Q, int k) {
 size_t nk_fwd_lds(int Q, int k, int ns) { return std::max<size_t>(16, ((size_t)k * Q + (size_t)ns * Q) * kWave * 4); }
 size_t nk_bwd_lds(int Q, int k, int ns) { return std::max<size_t>(16, (size_t)(1 + ns) * k * Q * kWave * 4); }
 
-void launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits) {
+// logits of every (parent, site); with `ce` on the small-grid path the
+// cross-entropy runs in the same launch (returns true: no logits written)
+bool launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits,
+                   const NkCe* ce = nullptr) {
   if (nk_use_small(a.R, a.L, a.Q, a.k, a.QK)) {
     const dim3 sgrid(a.L, (a.R + kNkSmallP - 1) / kNkSmallP);
     const size_t slds = nk_small_lds(a.Q, a.k, a.QK, false);
-    switch (a.Q) {
-      case 2: hipLaunchKernelGGL(nk_logits_small_kernel<2>, sgrid, dim3(kNkSmallThreads), slds, st, a, logits); break;
-      case 4: hipLaunchKernelGGL(nk_logits_small_kernel<4>, sgrid, dim3(kNkSmallThreads), slds, st, a, logits); break;
-      default: hipLaunchKernelGGL(nk_logits_small_kernel<0>, sgrid, dim3(kNkSmallThreads), slds, st, a, logits);
+    const NkCe c = ce ? *ce : NkCe{};
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, sgrid, dim3(kNkSmallThreads), slds, st, a, logits, c);
+    };
+    if (ce) {
+      switch (a.Q) {
+        case 2: go(nk_logits_small_kernel<2, true>); break;
+        case 4: go(nk_logits_small_kernel<4, true>); break;
+        default: go(nk_logits_small_kernel<0, true>);
+      }
+    } else {
+      switch (a.Q) {
+        case 2: go(nk_logits_small_kernel<2, false>); break;
+        case 4: go(nk_logits_small_kernel<4, false>); break;
+        default: go(nk_logits_small_kernel<0, false>);
+      }
     }
-    return;
+    return ce != nullptr;
   }
   const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);
   const size_t lds = nk_fwd_lds(a.Q, a.k, ns);
@@ -627,6 +669,7 @@ void launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits) {
     case 20: hipLaunchKernelGGL(nk_logits_kernel<20>, grid, block, lds, st, a, logits); break;
     default: hipLaunchKernelGGL(nk_logits_kernel<0>, grid, block, lds, st, a, logits);
   }
+  return false;
 }
 
 void launch_logits_bwd(const NkArgs& a, int ns, hipStream_t st, const float* g, float* G) {
@@ -816,13 +859,14 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
 
   NkArgs a{seqs, v.prow, interactions, fitness, n_parents, L, Q, k, (int)ipow(Q, k)};
   const int ns = nk_slices(n_parents, L, Q, k);
-  launch_logits(a, ns, st, logits);
-  if (int e = nk_err(fn)) return e;
   const double norm = (double)n_nonroot * (double)n_valid;
   const float scale = (float)((double)lambda_val / norm);
-  hipLaunchKernelGGL(nk_ce_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
-                     seqs, logits, v.cofs, v.cidx, seq_mask, n_parents, L, Q, scale, dlog, dchild,
-                     part);
+  const NkCe ce{seqs, v.cofs, v.cidx, seq_mask, scale, dlog, dchild, part};
+  if (!launch_logits(a, ns, st, logits, &ce))
+    hipLaunchKernelGGL(nk_ce_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
+                       seqs, logits, v.cofs, v.cidx, seq_mask, n_parents, L, Q, scale, dlog,
+                       dchild, part);
+  if (int e = nk_err(fn)) return e;
   // few (parent, site) partials (the eval shape: 465): one block sums them
   // directly; otherwise two fixed levels (chunks, then the chunk sums)
   const int64_t nparts = (int64_t)n_parents * L;
