@@ -2497,7 +2497,7 @@ extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t 
   // v5 f32 (one wave per SIMD, K % 4 == 0: 16-B rows); TREX_MF=3 or a
   // ragged K: the one-wave-per-tile kernel
   const char* ev = std::getenv("TREX_MF");
-  if (K % 4 == 0 && !(ev && std::atoi(ev) == 3))
+  if (K % 4 == 0 && 32LL * K * 4 < 0x7FFFFFF0LL && !(ev && std::atoi(ev) == 3))
     return mf_x3("trex_tree_mf_rows", M, S, N, K, row0, nrows, 1.0f, 1.0f, dS_rows, nullptr, 0,
                  stream, false);
   const int nrowt = (nrows + 63) / 64;
@@ -2547,7 +2547,11 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
   const int lds = 2 * (2 * 32 * 320 + 256 * kMfStride);
   const bool codes = codesR && lcs > 0;
   const char* ev = std::getenv("TREX_MF");
-  if (!x3 || !(ev && std::atoi(ev) == 3)) {  // v5 (default); TREX_MF=3 keeps v3 (x3 only)
+  // v5's dropped stores carry an out-of-bounds voffset plus a row soffset
+  // (< 32 K * 4 bytes): kept below 2^31 so the sum cannot wrap in bounds
+  const bool v5_ok = 32LL * K * 4 < 0x7FFFFFF0LL;
+  if (!x3 && !v5_ok) return set_error(TREX_E_UNSUPPORTED, "%s: K too large for the f32 v5 MF", fn);
+  if (v5_ok && (!x3 || !(ev && std::atoi(ev) == 3))) {  // v5 (default); TREX_MF=3 keeps v3
     // f32: the transposed F slice is CW x 144 B
     const int lds5 = x3 ? lds : 2 * (160 * kMfStride + 256 * kMfStride);
     auto go5 = [&](auto kernel, int tpc) {
