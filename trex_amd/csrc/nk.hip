@@ -334,176 +334,149 @@ __device__ __forceinline__ void nk_ce_one(const NkCe& c, const float (&xv)[kNkMa
   c.part[t] = ce;
 }
 
-constexpr int kNkSmallThreads = 256;
-constexpr int kNkSlices = 8;
-constexpr int kNkSmallP = kNkSmallThreads / kNkSlices;  // parents per block
+// ---- few (parent, site) pairs (the reference's eval shape: 31 x 15, Q = 2,
+// K = 10): one workgroup per pair, its threads over the Q^k joint states.
+// The wave-per-64-parents kernels above walk every joint state serially per
+// lane (serial chains of dependent table reads: 49 / 78 us for 2 M MACs);
+// here each thread takes joint states t, t + 256, ...: the product over the
+// k neighbours left to right (the reference's successive outer products),
+// F[s][idx] times it, and the block sums its threads in a fixed tree order.
+constexpr int kNkPP = 256;  // threads per (parent, site) workgroup
 
-struct SmallWalk {
-  int lo, hi;  // joint states [lo, hi) of this thread's slice
-};
-__device__ __forceinline__ SmallWalk small_walk(int QK, int sl) {
-  const int per = (QK + kNkSlices - 1) / kNkSlices;
-  SmallWalk w;
-  w.lo = min(QK, sl * per);
-  w.hi = min(QK, w.lo + per);
-  return w;
-}
-// digits of idx, neighbour 0 most significant
-__device__ __forceinline__ void small_digits(int idx, int k, int Q, int (&d)[kNkMaxK]) {
-#pragma unroll
-  for (int j = kNkMaxK - 1; j >= 0; --j) {
-    if (j < k) {
-      d[j] = idx % Q;
-      idx /= Q;
-    } else {
-      d[j] = 0;
-    }
-  }
-}
-__device__ __forceinline__ void small_next(int (&d)[kNkMaxK], int k, int Q) {
-  for (int j = k - 1; j >= 0; --j) {
-    if (++d[j] < Q) return;
-    d[j] = 0;
-  }
+// digits of idx, neighbour 0 most significant (Q = 2: shifts)
+template <int QT>
+__device__ __forceinline__ int nk_digit(int idx, int j, int k, int Q) {
+  if constexpr (QT == 2) return (idx >> (k - 1 - j)) & 1;
+  int v = idx;
+  for (int t = k - 1; t > j; --t) v /= Q;
+  return v % Q;
 }
 
-// stage the site's table F [Q][QK] and the block's parents' neighbour
-// distributions P [kNkSmallP][k][Q] into LDS
-__device__ __forceinline__ void small_stage(const NkArgs& a, int site, int p0, float* Fl, float* Pl) {
-  const int QK = a.QK, Q = a.Q, k = a.k;
-  const float* F = a.F + (size_t)site * QK * Q;
-  for (int e = threadIdx.x; e < Q * QK; e += kNkSmallThreads) Fl[e] = F[e];
-  const int32_t* inter = a.inter + (size_t)site * k;
-  for (int e = threadIdx.x; e < kNkSmallP * k * Q; e += kNkSmallThreads) {
-    const int pp = e / (k * Q), jc = e - pp * k * Q, j = jc / Q, c = jc - j * Q;
-    const int r = p0 + pp;
-    Pl[e] = r < a.R ? a.S[((size_t)a.rows[r] * a.L + inter[j]) * Q + c] : 0.0f;
-  }
-}
-
-// CE: the parent's logits go straight into the cross-entropy of its
-// children (nk_ce_one, the nk_ce_kernel arithmetic) instead of to HBM
-template <int QT, bool CE>
-__global__ __launch_bounds__(kNkSmallThreads) void nk_logits_small_kernel(NkArgs a,
-                                                                         float* __restrict__ logits,
-                                                                         NkCe ce) {
-  constexpr int MQ = QT ? QT : kNkMaxQ;
-  const int Q = QT ? QT : a.Q;
-  const int k = a.k;
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  float* Fl = sh;                                 // [Q][QK]
-  float* Pl = Fl + (size_t)Q * a.QK;              // [P][k][Q]
-  float* red = Pl + (size_t)kNkSmallP * k * Q;    // [slices][P][Q]
-  const int site = blockIdx.x, p0 = blockIdx.y * kNkSmallP;
-  small_stage(a, site, p0, Fl, Pl);
+// fixed-order block sum of n values per thread (LDS red[n][kNkPP]); thread 0
+// gets the totals in out
+template <int NV>
+__device__ __forceinline__ void nk_block_sum(float (&v)[NV], int n, float* red) {
+  const int t = threadIdx.x;
+  for (int q = 0; q < n; ++q) red[q * kNkPP + t] = v[q];
   __syncthreads();
-  const int pp = threadIdx.x % kNkSmallP, sl = threadIdx.x / kNkSmallP;
-  const float* P = Pl + (size_t)pp * k * Q;
-  const SmallWalk w = small_walk(a.QK, sl);
+  for (int w = kNkPP / 2; w > 0; w >>= 1) {
+    if (t < w)
+      for (int q = 0; q < n; ++q) red[q * kNkPP + t] += red[q * kNkPP + t + w];
+    __syncthreads();
+  }
+  for (int q = 0; q < n; ++q) v[q] = red[q * kNkPP];
+}
+
+// the parent's k neighbour distributions at this site, P[j][c], into LDS
+__device__ __forceinline__ void nk_pp_stage(const NkArgs& a, int r, int site, float* P) {
+  const int32_t* inter = a.inter + (size_t)site * a.k;
+  for (int e = threadIdx.x; e < a.k * a.Q; e += kNkPP) {
+    const int j = e / a.Q, c = e - j * a.Q;
+    P[e] = a.S[((size_t)a.rows[r] * a.L + inter[j]) * a.Q + c];
+  }
+}
+
+template <int QT, bool CE>
+__global__ __launch_bounds__(kNkPP) void nk_logits_pp_kernel(NkArgs a, float* __restrict__ logits,
+                                                              NkCe ce) {
+  constexpr int MQ = QT ? QT : kNkMaxQ;
+  const int Q = QT ? QT : a.Q, k = a.k, QK = a.QK;
+  __shared__ float P[kNkMaxK * kNkMaxQ];
+  __shared__ float red[MQ * kNkPP];
+  const int site = blockIdx.x % a.L, r = blockIdx.x / a.L;
+  nk_pp_stage(a, r, site, P);
+  __syncthreads();
+  const float* F = a.F + (size_t)site * QK * Q;
   float acc[MQ];
 #pragma unroll
   for (int s = 0; s < MQ; ++s) acc[s] = 0.0f;
-  int d[kNkMaxK];
-  small_digits(w.lo, k, Q, d);
-  for (int idx = w.lo; idx < w.hi; ++idx) {
-    float prod = k > 0 ? P[d[0]] : 1.0f;  // k = 0: the table alone (one joint state)
-#pragma unroll
-    for (int j = 1; j < kNkMaxK; ++j)
-      if (j < k) prod = prod * P[j * Q + d[j]];
+  for (int idx = threadIdx.x; idx < QK; idx += kNkPP) {
+    float prod = k > 0 ? P[nk_digit<QT>(idx, 0, k, Q)] : 1.0f;
+    for (int j = 1; j < k; ++j) prod = prod * P[j * Q + nk_digit<QT>(idx, j, k, Q)];
 #pragma unroll
     for (int s = 0; s < MQ; ++s)
-      if (s < Q) acc[s] = fmaf(Fl[(size_t)s * a.QK + idx], prod, acc[s]);
-    small_next(d, k, Q);
+      if (s < Q) acc[s] = fmaf(F[(size_t)s * QK + idx], prod, acc[s]);
   }
+  nk_block_sum<MQ>(acc, Q, red);
+  if (threadIdx.x != 0) return;
+  if constexpr (CE) {
+    float xv[kNkMaxQ];
 #pragma unroll
-  for (int s = 0; s < MQ; ++s)
-    if (s < Q) red[((size_t)sl * kNkSmallP + pp) * Q + s] = acc[s];
-  __syncthreads();
-  const int r = p0 + pp;
-  if (sl != 0 || r >= a.R) return;
-  float xv[kNkMaxQ];
-#pragma unroll
-  for (int s = 0; s < kNkMaxQ; ++s) xv[s] = -INFINITY;
-  for (int s = 0; s < Q; ++s) {
-    float v = red[(size_t)pp * Q + s];
-    for (int y = 1; y < kNkSlices; ++y) v += red[((size_t)y * kNkSmallP + pp) * Q + s];
-    if constexpr (CE)
-      xv[s] = v;
-    else
-      logits[((size_t)r * a.L + site) * Q + s] = v;
+    for (int s = 0; s < kNkMaxQ; ++s) xv[s] = s < Q ? acc[s < MQ ? s : 0] : -INFINITY;
+    nk_ce_one(ce, xv, r, site, a.L, Q);
+  } else {
+    for (int s = 0; s < Q; ++s) logits[((size_t)r * a.L + site) * Q + s] = acc[s];
   }
-  if constexpr (CE) nk_ce_one(ce, xv, r, site, a.L, Q);
 }
 
+// reverse: w(idx) = sum_s g_s F[s][idx]; bin (j, c_j(idx)) += w * prod_{j' != j}
+// P[j'][c_j'] (prefix x suffix products), per-thread bins summed in a fixed
+// tree order; G[r][site][j][c]
 template <int QT>
-__global__ __launch_bounds__(kNkSmallThreads) void nk_logits_bwd_small_kernel(
-    NkArgs a, const float* __restrict__ g, float* __restrict__ G) {
+__global__ __launch_bounds__(kNkPP) void nk_logits_bwd_pp_kernel(NkArgs a,
+                                                                  const float* __restrict__ g,
+                                                                  float* __restrict__ G) {
   constexpr int MQ = QT ? QT : kNkMaxQ;
-  const int Q = QT ? QT : a.Q;
-  const int k = a.k, kq = k * Q;
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  float* Fl = sh;                                     // [Q][QK]
-  float* Pl = Fl + (size_t)Q * a.QK;                  // [P][k][Q]
-  float* gb = Pl + (size_t)kNkSmallP * kq;            // [threads][k][Q] bins
-  const int site = blockIdx.x, p0 = blockIdx.y * kNkSmallP;
-  small_stage(a, site, p0, Fl, Pl);
-  float* bins = gb + (size_t)threadIdx.x * kq;
-  for (int t = 0; t < kq; ++t) bins[t] = 0.0f;
+  constexpr int MB = QT ? kNkMaxK * QT : kNkMaxK * kNkMaxQ;  // bins per thread
+  const int Q = QT ? QT : a.Q, k = a.k, QK = a.QK;
+  __shared__ float P[kNkMaxK * kNkMaxQ];
+  extern __shared__ float redb[];  // [k * Q][kNkPP]
+  const int site = blockIdx.x % a.L, r = blockIdx.x / a.L;
+  nk_pp_stage(a, r, site, P);
   __syncthreads();
-  const int pp = threadIdx.x % kNkSmallP, sl = threadIdx.x / kNkSmallP;
-  const int r = p0 + pp;
-  const float* P = Pl + (size_t)pp * kq;
+  const float* F = a.F + (size_t)site * QK * Q;
   float gs[MQ];
 #pragma unroll
-  for (int s = 0; s < MQ; ++s) gs[s] = (s < Q && r < a.R) ? g[((size_t)r * a.L + site) * Q + s] : 0.0f;
-  const SmallWalk w = small_walk(a.QK, sl);
-  int d[kNkMaxK];
-  small_digits(w.lo, k, Q, d);
-  for (int idx = w.lo; idx < w.hi; ++idx) {
-    float dj = 0.0f;
+  for (int s = 0; s < MQ; ++s) gs[s] = s < Q ? g[((size_t)r * a.L + site) * Q + s] : 0.0f;
+  float bins[MB];
+#pragma unroll
+  for (int b = 0; b < MB; ++b) bins[b] = 0.0f;
+  for (int idx = threadIdx.x; idx < QK; idx += kNkPP) {
+    float w = 0.0f;
 #pragma unroll
     for (int s = 0; s < MQ; ++s)
-      if (s < Q) dj = fmaf(gs[s], Fl[(size_t)s * a.QK + idx], dj);
-    float f[kNkMaxK], E[kNkMaxK];
-#pragma unroll
-    for (int j = 0; j < kNkMaxK; ++j) f[j] = j < k ? P[j * Q + d[j]] : 1.0f;
-    float pre = 1.0f;
+      if (s < Q) w = fmaf(gs[s], F[(size_t)s * QK + idx], w);
+    int c[kNkMaxK];
+    float pre[kNkMaxK];
+    float acc = 1.0f;
 #pragma unroll
     for (int j = 0; j < kNkMaxK; ++j) {
-      E[j] = pre;
-      pre *= f[j];
+      if (j < k) {
+        c[j] = nk_digit<QT>(idx, j, k, Q);
+        pre[j] = acc;
+        acc = acc * P[j * Q + c[j]];
+      }
     }
     float suf = 1.0f;
 #pragma unroll
     for (int j = kNkMaxK - 1; j >= 0; --j) {
-      E[j] *= suf;
-      suf *= f[j];
-    }
+      if (j < k) {
+        const float v = w * (pre[j] * suf);
 #pragma unroll
-    for (int j = 0; j < kNkMaxK; ++j)
-      if (j < k) bins[j * Q + d[j]] = fmaf(dj, E[j], bins[j * Q + d[j]]);
-    small_next(d, k, Q);
+        for (int q = 0; q < MQ; ++q)
+          if (q == c[j]) bins[j * MQ + q] += v;
+        suf = suf * P[j * Q + c[j]];
+      }
+    }
   }
+  // fixed-order tree sum of the k * Q bins over the threads
+  const int t = threadIdx.x;
+  const int nbin = k * Q;
+  for (int j = 0; j < k; ++j)
+    for (int q = 0; q < Q; ++q) redb[(j * Q + q) * kNkPP + t] = bins[j * MQ + (q < MQ ? q : 0)];
   __syncthreads();
-  if (sl != 0 || r >= a.R) return;
-  float* o = G + (((size_t)r * a.L + site) * k) * Q;
-  for (int t = 0; t < kq; ++t) {
-    float v = gb[(size_t)pp * kq + t];
-    for (int y = 1; y < kNkSlices; ++y) v += gb[((size_t)(y * kNkSmallP + pp)) * kq + t];
-    o[t] = v;
+  for (int w = kNkPP / 2; w > 0; w >>= 1) {
+    if (t < w)
+      for (int b = 0; b < nbin; ++b) redb[b * kNkPP + t] += redb[b * kNkPP + t + w];
+    __syncthreads();
   }
+  for (int b = t; b < nbin; b += kNkPP) G[((size_t)r * a.L + site) * nbin + b] = redb[b * kNkPP];
 }
 
-// the small-grid kernels serve grids of few (parent group, site) blocks whose
-// staged table, parents and bins fit 64 KiB of LDS
-size_t nk_small_lds(int Q, int k, int QK, bool bwd) {
-  return ((size_t)Q * QK + (size_t)kNkSmallP * k * Q +
-          (bwd ? (size_t)kNkSmallThreads * k * Q : (size_t)kNkSlices * kNkSmallP * Q)) * 4;
-}
-bool nk_use_small(int R, int L, int Q, int k, int QK) {
-  if (k == 0) return false;
-  const int64_t blocks_wave = (int64_t)((R + kWave - 1) / kWave) * L;
-  return blocks_wave < 256 && nk_small_lds(Q, k, QK, true) <= 65536;
+// the per-pair kernels for few (parent, site) pairs with many joint states
+bool nk_use_pp(int R, int L, int Q, int k, int QK) {
+  if (k == 0 || (Q != 2 && Q != 4)) return false;
+  return (int64_t)R * L <= 4096 && QK >= kNkPP;
 }
 
 
@@ -639,25 +612,16 @@ size_t nk_bwd_lds(int Q, int k, int ns) { return std::max<size_t>(16, (size_t)(1
 // cross-entropy runs in the same launch (returns true: no logits written)
 bool launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits,
                    const NkCe* ce = nullptr) {
-  if (nk_use_small(a.R, a.L, a.Q, a.k, a.QK)) {
-    const dim3 sgrid(a.L, (a.R + kNkSmallP - 1) / kNkSmallP);
-    const size_t slds = nk_small_lds(a.Q, a.k, a.QK, false);
+  if (nk_use_pp(a.R, a.L, a.Q, a.k, a.QK)) {
+    const dim3 grid((unsigned)((int64_t)a.R * a.L));
     const NkCe c = ce ? *ce : NkCe{};
-    auto go = [&](auto kern) {
-      hipLaunchKernelGGL(kern, sgrid, dim3(kNkSmallThreads), slds, st, a, logits, c);
-    };
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kNkPP), 0, st, a, logits, c); };
     if (ce) {
-      switch (a.Q) {
-        case 2: go(nk_logits_small_kernel<2, true>); break;
-        case 4: go(nk_logits_small_kernel<4, true>); break;
-        default: go(nk_logits_small_kernel<0, true>);
-      }
+      if (a.Q == 2) go(nk_logits_pp_kernel<2, true>);
+      else go(nk_logits_pp_kernel<4, true>);
     } else {
-      switch (a.Q) {
-        case 2: go(nk_logits_small_kernel<2, false>); break;
-        case 4: go(nk_logits_small_kernel<4, false>); break;
-        default: go(nk_logits_small_kernel<0, false>);
-      }
+      if (a.Q == 2) go(nk_logits_pp_kernel<2, false>);
+      else go(nk_logits_pp_kernel<4, false>);
     }
     return ce != nullptr;
   }
@@ -673,14 +637,13 @@ bool launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits,
 }
 
 void launch_logits_bwd(const NkArgs& a, int ns, hipStream_t st, const float* g, float* G) {
-  if (nk_use_small(a.R, a.L, a.Q, a.k, a.QK)) {
-    const dim3 sgrid(a.L, (a.R + kNkSmallP - 1) / kNkSmallP);
-    const size_t slds = nk_small_lds(a.Q, a.k, a.QK, true);
-    switch (a.Q) {
-      case 2: hipLaunchKernelGGL(nk_logits_bwd_small_kernel<2>, sgrid, dim3(kNkSmallThreads), slds, st, a, g, G); break;
-      case 4: hipLaunchKernelGGL(nk_logits_bwd_small_kernel<4>, sgrid, dim3(kNkSmallThreads), slds, st, a, g, G); break;
-      default: hipLaunchKernelGGL(nk_logits_bwd_small_kernel<0>, sgrid, dim3(kNkSmallThreads), slds, st, a, g, G);
-    }
+  if (nk_use_pp(a.R, a.L, a.Q, a.k, a.QK)) {
+    const dim3 grid((unsigned)((int64_t)a.R * a.L));
+    const size_t lds = (size_t)a.k * a.Q * kNkPP * 4;
+    if (a.Q == 2)
+      hipLaunchKernelGGL(nk_logits_bwd_pp_kernel<2>, grid, dim3(kNkPP), lds, st, a, g, G);
+    else
+      hipLaunchKernelGGL(nk_logits_bwd_pp_kernel<4>, grid, dim3(kNkPP), lds, st, a, g, G);
     return;
   }
   const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);

@@ -855,43 +855,62 @@ __global__ void step_advance_kernel(StepState* __restrict__ st, float b1, float 
   }
 }
 
-// The whole surrogate for small trees (N <= 64, N K <= 8192: the NK eval
+// The whole surrogate for small trees (N <= 64, N K <= 4096: the NK eval
 // shape is 63 x 30) in one workgroup: S, G = S S^T and M in LDS, G by
 // fp32 fmaf over k in order (i <= j computed, mirrored: exactly symmetric),
 // the combine's rows in fp64 (thread i sums row i over j in order), the
 // loss summed over rows in order by thread 0, dS = M S.  One launch where
 // the general path takes five (Gram, its reduce, combine, row sum, MF).
 constexpr int kSurSmallN = 64;
-constexpr int kSurSmallNK = 8192;
-__global__ __launch_bounds__(256) void surrogate_small_kernel(const float* __restrict__ S,
-                                                             const float* __restrict__ A, int N,
-                                                             int K, float* __restrict__ loss,
-                                                             float* __restrict__ dS,
-                                                             float* __restrict__ dA,
-                                                             float* __restrict__ G_out) {
+constexpr int kSurSmallNK = 4096;
+__global__ __launch_bounds__(1024) void surrogate_small_kernel(const float* __restrict__ S,
+                                                              const float* __restrict__ A, int N,
+                                                              int K, float* __restrict__ loss,
+                                                              float* __restrict__ dS,
+                                                              float* __restrict__ dA,
+                                                              float* __restrict__ G_out) {
+  constexpr int T = 1024;
   __shared__ float sS[kSurSmallNK];
   __shared__ float sG[kSurSmallN * kSurSmallN];
   __shared__ float sM[kSurSmallN * kSurSmallN];
+  __shared__ float sA[kSurSmallN * kSurSmallN];
+  __shared__ double part[3][kSurSmallN * 4];  // row loss, row sum, column sum partials
   __shared__ double rl[kSurSmallN];
   const int tid = threadIdx.x;
-  for (int e = tid; e < N * K; e += 256) sS[e] = S[e];
+  // every operand into LDS first, all loads in flight together; each sum
+  // below runs four independent partial chains combined in a fixed order (a
+  // serial chain of LDS reads per entry left the block latency-bound)
+  for (int e = tid; e < N * K; e += T) sS[e] = S[e];
+  for (int e = tid; e < N * N; e += T) sA[e] = A[e];
   __syncthreads();
-  for (int e = tid; e < N * N; e += 256) {
+  auto dot4 = [](const float* x, int sx, const float* y, int sy, int n) {
+    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, c3 = 0.0f;
+    int t = 0;
+    for (; t + 3 < n; t += 4) {
+      c0 = fmaf(x[t * sx], y[t * sy], c0);
+      c1 = fmaf(x[(t + 1) * sx], y[(t + 1) * sy], c1);
+      c2 = fmaf(x[(t + 2) * sx], y[(t + 2) * sy], c2);
+      c3 = fmaf(x[(t + 3) * sx], y[(t + 3) * sy], c3);
+    }
+    for (; t < n; ++t) c0 = fmaf(x[t * sx], y[t * sy], c0);
+    return (c0 + c1) + (c2 + c3);
+  };
+  for (int e = tid; e < N * N; e += T) {
     const int i = e / N, j = e - i * N;
     if (i > j) continue;
-    float g = 0.0f;
-    for (int k = 0; k < K; ++k) g = fmaf(sS[i * K + k], sS[j * K + k], g);
+    const float g = dot4(sS + i * K, 1, sS + j * K, 1, K);
     sG[i * N + j] = g;
     sG[j * N + i] = g;
   }
   __syncthreads();
-  if (tid < N) {
-    const int i = tid;
+  // combine: row i over 4 threads (j = q, q + 4, ...), fp64 partials
+  if (tid < 4 * N) {
+    const int i = tid >> 2, q = tid & 3;
     const float gii = sG[i * N + i];
     double l = 0.0, rs = 0.0, cs = 0.0;
-    for (int j = 0; j < N; ++j) {
-      const float a = A[(size_t)i * N + j];
-      const float at = A[(size_t)j * N + i];
+    for (int j = q; j < N; j += 4) {
+      const float a = sA[i * N + j];
+      const float at = sA[j * N + i];
       const float gjj = sG[j * N + j];
       const float gij = sG[i * N + j];
       l += (double)a * ((double)gii + (double)gjj - 2.0 * (double)gij);
@@ -900,25 +919,33 @@ __global__ __launch_bounds__(256) void surrogate_small_kernel(const float* __res
       if (dA) dA[(size_t)i * N + j] = 0.5f * (gii + gjj) - gij;
       sM[i * N + j] = -(a + at);
     }
-    sM[i * N + i] += (float)(rs + cs);
-    rl[i] = 0.5 * l;
+    part[0][tid] = l;
+    part[1][tid] = rs;
+    part[2][tid] = cs;
   }
   if (G_out)
-    for (int e = tid; e < N * N; e += 256) G_out[e] = sG[e];
+    for (int e = tid; e < N * N; e += T) G_out[e] = sG[e];
+  __syncthreads();
+  if (tid < N) {
+    const int i = tid;
+    const double* p0 = part[0] + 4 * i;
+    const double* p1 = part[1] + 4 * i;
+    const double* p2 = part[2] + 4 * i;
+    rl[i] = 0.5 * (((p0[0] + p0[1]) + p0[2]) + p0[3]);
+    const double rc = (((p1[0] + p1[1]) + p1[2]) + p1[3]) + (((p2[0] + p2[1]) + p2[2]) + p2[3]);
+    sM[i * N + i] += (float)rc;
+  }
   __syncthreads();
   if (tid == 0) {
     double t = 0.0;
     for (int i = 0; i < N; ++i) t += rl[i];
     loss[0] = (float)t;
   }
-  if (dS) {
-    for (int e = tid; e < N * K; e += 256) {
+  if (dS)
+    for (int e = tid; e < N * K; e += T) {
       const int n = e / K, k = e - n * K;
-      float v = 0.0f;
-      for (int j = 0; j < N; ++j) v = fmaf(sM[n * N + j], sS[j * K + k], v);
-      dS[e] = v;
+      dS[e] = dot4(sM + n * N, 1, sS + k, K, N);
     }
-  }
 }
 
 __global__ __launch_bounds__(256) void sum_rows_kernel(const double* __restrict__ v, int n,
@@ -2024,10 +2051,14 @@ Gram3Plan gram5_plan(int N, int64_t K, int t0s, int* T) {
   g.ksplit = std::max(1, std::min(g.nchunks, ks));
   return g;
 }
-// v5 by default; TREX_GRAM=3 keeps v3 (A/B timing)
-bool gram5_on() {
+// kernel version per precision: f32 -> v5 (one wave per SIMD: the 64-cycle
+// f32 MFMAs fill the pipe; 587 -> 397 us at C5), x3 -> v3 (two waves per
+// SIMD: the f16 MFMA chains need the second wave; v5 measured 231 vs 152
+// us).  TREX_GRAM=3 / 5 forces one version for both (A/B).
+int gram_version(bool x3) {
   const char* e = std::getenv("TREX_GRAM");
-  return !(e && std::atoi(e) == 3);
+  if (e && (std::atoi(e) == 3 || std::atoi(e) == 5)) return std::atoi(e);
+  return x3 ? 3 : 5;
 }
 bool gram3_ok(int N, int64_t K) { return N <= kG3Rows && K % 4 == 0 && (int64_t)N * K * 4 < 0x7FFFFFF0LL; }
 }  // namespace
@@ -2079,9 +2110,10 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
   const int blocks = g.npairs * ks8;
   // v5 serves both precisions; v3 (TREX_GRAM=3) only the x3 one
   const bool x3 = x3_max > 0.0f;
-  if (symmetric && X == Y && gram3_ok(N, K) && (x3 || gram5_on())) {
+  const int gv = gram_version(x3);
+  if (symmetric && X == Y && gram3_ok(N, K) && (x3 || gv == 5)) {
     int T5 = 0;
-    const bool v5 = gram5_on();
+    const bool v5 = gv == 5;
     const Gram3Plan p = v5 ? gram5_plan(N, K, 2 * t0, &T5) : gram3_plan(N, K, 2 * t0);
     if (p.ntiles == 0) return TREX_OK;
     static bool lds_set = false;
@@ -2172,7 +2204,7 @@ extern "C" int trex_tree_surrogate(const float* S, const float* A, int N, int64_
   w += (int64_t)N * N * 4;
   double* rowloss = reinterpret_cast<double*>(w);
   if (N <= kSurSmallN && (int64_t)N * K <= kSurSmallNK) {
-    hipLaunchKernelGGL(surrogate_small_kernel, dim3(1), dim3(256), 0, st, S, A, N, (int)K, loss,
+    hipLaunchKernelGGL(surrogate_small_kernel, dim3(1), dim3(1024), 0, st, S, A, N, (int)K, loss,
                        dS, dA, G_out);
     return tree_hip_check("trex_tree_surrogate");
   }
@@ -2494,8 +2526,8 @@ extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t 
     return set_error(TREX_E_ARG, "trex_tree_mf_rows: bad arguments");
   if ((int64_t)N * K * 4 > 0x7FFFFFF0LL)
     return set_error(TREX_E_UNSUPPORTED, "trex_tree_mf_rows: S exceeds 2 GiB");
-  // v5 f32 (one wave per SIMD, K % 4 == 0: 16-B rows); TREX_MF=3 or a
-  // ragged K: the one-wave-per-tile kernel
+  // v5 f32 (one wave per SIMD, K % 4 == 0: 16-B rows; 525 -> 467 us at C5);
+  // TREX_MF=3 or a ragged K: the one-wave-per-tile kernel
   const char* ev = std::getenv("TREX_MF");
   if (K % 4 == 0 && 32LL * K * 4 < 0x7FFFFFF0LL && !(ev && std::atoi(ev) == 3))
     return mf_x3("trex_tree_mf_rows", M, S, N, K, row0, nrows, 1.0f, 1.0f, dS_rows, nullptr, 0,
@@ -2551,7 +2583,8 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
   // (< 32 K * 4 bytes): kept below 2^31 so the sum cannot wrap in bounds
   const bool v5_ok = 32LL * K * 4 < 0x7FFFFFF0LL;
   if (!x3 && !v5_ok) return set_error(TREX_E_UNSUPPORTED, "%s: K too large for the f32 v5 MF", fn);
-  if (v5_ok && (!x3 || !(ev && std::atoi(ev) == 3))) {  // v5 (default); TREX_MF=3 keeps v3
+  // f32: v5; x3: v3 (v5 measured 242 vs 224 us with leaf codes at C5) unless TREX_MF=5
+  if (v5_ok && (!x3 || (ev && std::atoi(ev) == 5))) {
     // f32: the transposed F slice is CW x 144 B
     const int lds5 = x3 ? lds : 2 * (160 * kMfStride + 256 * kMfStride);
     auto go5 = [&](auto kernel, int tpc) {
