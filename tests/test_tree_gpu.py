@@ -230,9 +230,10 @@ def test_tree_optimizer_x3_needs_aligned_rows_and_says_so(device):
     assert opt.gemm == "f32"
 
 
-@pytest.fixture(params=["5", "3"])
+@pytest.fixture(params=["5", "3", "6"])
 def gram_version(request, monkeypatch):
-    """The x3 Gram / MF kernels: v5 (default) and v3 (TREX_GRAM=3, TREX_MF=3)."""
+    """Every Gram / MF kernel version: v5 (one wave per SIMD; the f32 default),
+    v3 (the x3 default), v6 (the x3 Gram at two waves per SIMD, A/B)."""
     monkeypatch.setenv("TREX_GRAM", request.param)
     monkeypatch.setenv("TREX_MF", request.param)
     return request.param

@@ -42,30 +42,44 @@ if __name__ == "__main__":
         return e0.elapsed_time(e1) / reps * 1e3
 
     mx = float(N + 1) * 50
-    tg0 = timed(lambda: check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, nl, 1.0, ptr(G0), ptr(ws),
-                                                           ws.numel(), st)))
-    tm0 = timed(lambda: check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, nl, N - nl, mx, 1.0,
-                                                         ptr(d0), st)))
-    tm1 = timed(lambda: check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, N - nl, mx,
-                                                               1.0, ptr(cb), cb.numel(), nl, 4,
-                                                               ptr(d1), st)))
-    os.environ["TREX_GRAM"] = "3"
-    G3 = torch.zeros((N, N), device=dev)
-    tg3 = timed(lambda: check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, nl, 1.0, ptr(G3), ptr(ws),
-                                                           ws.numel(), st)))
-    os.environ["TREX_GRAM"] = "5"
-    os.environ["TREX_MF"] = "3"
-    d3 = torch.empty((N - nl, K), device=dev)
-    tm3 = timed(lambda: check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl, N - nl, mx,
-                                                               1.0, ptr(cb), cb.numel(), nl, 4,
-                                                               ptr(d3), st)))
-    os.environ["TREX_MF"] = "5"
-    print(f"mf(codes) v3 {tm3:.1f} us  bitwise v5 == v3 {torch.equal(d1, d3)}")
-    # exact f32 GEMMs (TreeOptimizer(gemm="f32")): v5 against the older kernels
+
+    def setv(gram=None, mf=None):
+        for key, v in (("TREX_GRAM", gram), ("TREX_MF", mf)):
+            if v is None:
+                os.environ.pop(key, None)
+            else:
+                os.environ[key] = v
+
+    # x3 Gram: every kernel version (v3 default, v5 one wave per SIMD, v6 two)
+    gx = {}
+    for ver in ("3", "5", "6"):
+        setv(gram=ver)
+        Gv = torch.zeros((N, N), device=dev)
+        tv = timed(lambda: check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, nl, 1.0, ptr(Gv),
+                                                              ptr(ws), ws.numel(), st)))
+        gx[ver] = (tv, Gv)
+    G3 = gx["3"][1]
+    for ver in ("5", "6"):
+        gd = ((gx[ver][1] - G3).abs()[nl:] / G3.abs()[nl:].clamp_min(1e-30)).max().item()
+        print(f"x3 gram v{ver} {gx[ver][0]:.1f} us vs v3 {gx['3'][0]:.1f} us (max rel diff {gd:.3g})")
+    # x3 MF (f32 rows, leaf codes): v3 default, v5
+    mfx = {}
+    for ver in ("3", "5"):
+        setv(mf=ver)
+        tm0 = timed(lambda: check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, nl, N - nl, mx,
+                                                             1.0, ptr(d0), st)))
+        tm1 = timed(lambda: check(lib().trex_tree_mf_rows_x3_codes(ptr(M), ptr(S), N, K, nl,
+                                                                   N - nl, mx, 1.0, ptr(cb),
+                                                                   cb.numel(), nl, 4, ptr(d1),
+                                                                   st)))
+        mfx[ver] = (tm0, tm1, torch.equal(d0, d1), d1.clone())
+    print(f"x3 mf v3 {mfx['3'][0]:.1f} us (codes {mfx['3'][1]:.1f}), v5 {mfx['5'][0]:.1f} us "
+          f"(codes {mfx['5'][1]:.1f}); codes bitwise rows {mfx['3'][2]} / {mfx['5'][2]}; "
+          f"v5 == v3 {torch.equal(mfx['3'][3], mfx['5'][3])}")
+    # exact f32 GEMMs (TreeOptimizer(gemm="f32")): v5 default against the older kernels
     f32 = {}
     for ver in ("5", "3"):
-        os.environ["TREX_GRAM"] = ver
-        os.environ["TREX_MF"] = ver
+        setv(gram=ver, mf=ver)
         Gf = torch.zeros((N, N), device=dev)
         df = torch.empty((N - nl, K), device=dev)
         tg = timed(lambda: check(lib().trex_tree_gram_skip(ptr(S), N, K, nl, ptr(Gf), ptr(ws),
@@ -73,15 +87,8 @@ if __name__ == "__main__":
         tm = timed(lambda: check(lib().trex_tree_mf_rows(ptr(M), ptr(S), N, K, nl, N - nl,
                                                          ptr(df), st)))
         f32[ver] = (tg, tm, Gf, df)
-    os.environ["TREX_GRAM"] = "5"
-    os.environ["TREX_MF"] = "5"
+    setv()
     gr = ((f32["5"][2] - f32["3"][2]).abs()[nl:] / f32["3"][2].abs()[nl:].clamp_min(1e-30)).max()
     mr = ((f32["5"][3] - f32["3"][3]).abs() / (M[nl:].abs() @ S.abs()).clamp_min(1e-30)).max()
     print(f"f32 gram v5 {f32['5'][0]:.1f} us  v3 {f32['3'][0]:.1f} us (max rel diff {gr.item():.3g}); "
           f"f32 mf v5 {f32['5'][1]:.1f} us  old {f32['3'][1]:.1f} us (max diff / |M||S| {mr.item():.3g})")
-    gd = ((G0 - G3).abs()[nl:] / G3.abs()[nl:].clamp_min(1e-30)).max().item()
-    print(f"gram v5 {tg0:.1f} us  gram v3 {tg3:.1f} us  (max rel diff v5 vs v3 {gd:.3g})")
-    deq = torch.equal(d0, d1)
-    dd = (d0 - d1).abs().max().item()
-    print(f"gram {tg0:.1f} us  mf {tm0:.1f} us  mf(codes) {tm1:.1f} us  bitwise dS {deq} "
-          f"(max diff {dd:.3g})")

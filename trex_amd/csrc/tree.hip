@@ -641,8 +641,10 @@ constexpr int kG5MaxTiles = 16;
 
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 
-template <int T, bool X3>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gram_kernel5(
+// W = 8 (two waves per SIMD, T <= 8 tiles each: 128 accumulator registers)
+// is the x3 variant under test (TREX_GRAM=6)
+template <int T, bool X3, int W = kG5Waves>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4, W / 4))) void gram_kernel5(
     const float* __restrict__ S, int N, int K, int ns, int t0s, int ntiles, int ngroups,
     int ksplit, int nchunks, float sc, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds5[];
@@ -655,7 +657,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int tb = (g * kG5Waves + wave) * T;
+  const int tb = (g * W + wave) * T;
   const int nt = max(0, min(T, ntiles - tb));
   // per-slot strip byte offsets (wave-uniform); slots past the wave's range
   // repeat the last strips and are not stored
@@ -680,7 +682,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   const rsrc_t rs = make_rsrc(S, (uint32_t)((size_t)N * K * 4));
   const int sub = tid & 3, rb = tid >> 2;
-  constexpr int kRowsPerPass = kG5Waves * kWave / 4;  // 64
+  constexpr int kRowsPerPass = W * kWave / 4;  // 64 (W = 4) / 128 (W = 8)
   constexpr int kPasses = kG3Rows / kRowsPerPass;     // 8
   u32x4 pf[kPasses];
   auto gload1 = [&](int i, int c) {
@@ -2042,10 +2044,11 @@ Gram3Plan gram3_plan(int N, int64_t K, int t0s) {
 }
 // v5: ngroups = ceil(ntiles / 64), T = tiles per wave; ksplit a multiple of
 // 8 (the XCD pairing of a split's groups), about one workgroup per CU
-Gram3Plan gram5_plan(int N, int64_t K, int t0s, int* T) {
+Gram3Plan gram5_plan(int N, int64_t K, int t0s, int* T, int W = kG5Waves) {
   Gram3Plan g = gram3_plan(N, K, t0s);
-  g.ngroups = std::max(1, (g.ntiles + kG5Waves * kG5MaxTiles - 1) / (kG5Waves * kG5MaxTiles));
-  *T = std::max(1, (g.ntiles + kG5Waves * g.ngroups - 1) / (kG5Waves * g.ngroups));
+  const int maxt = W == 8 ? 8 : kG5MaxTiles;
+  g.ngroups = std::max(1, (g.ntiles + W * maxt - 1) / (W * maxt));
+  *T = std::max(1, (g.ntiles + W * g.ngroups - 1) / (W * g.ngroups));
   int ks = std::max(1, 256 / g.ngroups);
   ks = std::max(8, ks / 8 * 8);
   g.ksplit = std::max(1, std::min(g.nchunks, ks));
@@ -2057,7 +2060,7 @@ Gram3Plan gram5_plan(int N, int64_t K, int t0s, int* T) {
 // us).  TREX_GRAM=3 / 5 forces one version for both (A/B).
 int gram_version(bool x3) {
   const char* e = std::getenv("TREX_GRAM");
-  if (e && (std::atoi(e) == 3 || std::atoi(e) == 5)) return std::atoi(e);
+  if (e && (std::atoi(e) == 3 || std::atoi(e) == 5 || std::atoi(e) == 6)) return std::atoi(e);
   return x3 ? 3 : 5;
 }
 bool gram3_ok(int N, int64_t K) { return N <= kG3Rows && K % 4 == 0 && (int64_t)N * K * 4 < 0x7FFFFFF0LL; }
@@ -2077,7 +2080,8 @@ int64_t part_bytes(int N, int64_t K) {
     const int ns = (N + 31) / 32;
     for (int t0s = 0; t0s <= ns; ++t0s) {
       int T5;
-      for (const Gram3Plan& g : {gram3_plan(N, K, t0s), gram5_plan(N, K, t0s, &T5)})
+      for (const Gram3Plan& g : {gram3_plan(N, K, t0s), gram5_plan(N, K, t0s, &T5),
+                                 gram5_plan(N, K, t0s, &T5, 8)})
         b = std::max<int64_t>(b, (int64_t)g.ksplit * g.ntiles * 4096);
     }
   }
@@ -2111,10 +2115,11 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
   // v5 serves both precisions; v3 (TREX_GRAM=3) only the x3 one
   const bool x3 = x3_max > 0.0f;
   const int gv = gram_version(x3);
-  if (symmetric && X == Y && gram3_ok(N, K) && (x3 || gv == 5)) {
+  if (symmetric && X == Y && gram3_ok(N, K) && (x3 || gv >= 5)) {
     int T5 = 0;
-    const bool v5 = gv == 5;
-    const Gram3Plan p = v5 ? gram5_plan(N, K, 2 * t0, &T5) : gram3_plan(N, K, 2 * t0);
+    const bool v5 = gv >= 5;
+    const int W = (gv == 6 && x3) ? 8 : kG5Waves;
+    const Gram3Plan p = v5 ? gram5_plan(N, K, 2 * t0, &T5, W) : gram3_plan(N, K, 2 * t0);
     if (p.ntiles == 0) return TREX_OK;
     static bool lds_set = false;
     if (!lds_set) {
@@ -2143,10 +2148,24 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
       }();
       (void)set5;
       auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, dim3(kG5Waves * kWave), kG3Lds, st, X, N, (int)K, p.ns,
+        hipLaunchKernelGGL(kern, grid, dim3(W * kWave), kG3Lds, st, X, N, (int)K, p.ns,
                            p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks, x3 ? sc : 1.0f, part);
       };
-      if (x3) {
+      static const bool set6 = [] {
+        for (const void* f : {reinterpret_cast<const void*>(gram_kernel5<4, true, 8>),
+                              reinterpret_cast<const void*>(gram_kernel5<6, true, 8>),
+                              reinterpret_cast<const void*>(gram_kernel5<7, true, 8>),
+                              reinterpret_cast<const void*>(gram_kernel5<8, true, 8>)})
+          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
+        return true;
+      }();
+      (void)set6;
+      if (x3 && W == 8) {
+        if (T5 <= 4) go(gram_kernel5<4, true, 8>);
+        else if (T5 <= 6) go(gram_kernel5<6, true, 8>);
+        else if (T5 <= 7) go(gram_kernel5<7, true, 8>);
+        else go(gram_kernel5<8, true, 8>);
+      } else if (x3) {
         if (T5 <= 4) go(gram_kernel5<4, true>);
         else if (T5 <= 8) go(gram_kernel5<8, true>);
         else if (T5 <= 10) go(gram_kernel5<10, true>);
