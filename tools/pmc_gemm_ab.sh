@@ -15,9 +15,10 @@ for v in 3 5; do
     mkdir -p $R/gpurun_out/pmcab/v$v
     TREX_GRAM=$v TREX_MF=$v timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $P -d $R/gpurun_out/pmcab/v$v/pass$i -o run --output-format csv -- python3 $R/tools/prof_gemm.py > $R/gpurun_out/pmcab/v$v/pass$i.log 2>&1
   done
-  for k in gram_kernel mf_kernel; do
+  for k in "gram_kernel3" "gram_kernel5<13, true" "gram_kernel5<13, false" "gram_kernel2<false" \
+           "mf_kernel3<5, false" "mf_kernel5<5, false, true" "mf_kernel5<5, false, false" "mf_kernel2<false"; do
     echo "== v$v $k" >> $R/gpurun_out/pmcab/summary.txt
-    python3 $R/tools/pmc_sum.py $R/gpurun_out/pmcab/v$v $k >> $R/gpurun_out/pmcab/summary.txt
+    python3 $R/tools/pmc_sum.py $R/gpurun_out/pmcab/v$v "$k" >> $R/gpurun_out/pmcab/summary.txt
   done
 done
 echo done

@@ -1,6 +1,7 @@
 """C5-shape GEMM kernels alone (for rocprofv3 --pmc passes): the f16x3 Gram
 (trex_tree_gram_skip_x3, leaf block skipped) and ancestor-rows MF
-(trex_tree_mf_rows_x3) at N = 511, K = 50 000 x 4, a few launches each."""
+(trex_tree_mf_rows_x3), then the f32 ones (trex_tree_gram_skip /
+trex_tree_mf_rows), at N = 511, K = 50 000 x 4, a few launches each."""
 import os
 import sys
 
@@ -25,5 +26,8 @@ if __name__ == "__main__":
         check(lib().trex_tree_gram_skip_x3(ptr(S), N, K, nl, 1.0, ptr(G), ptr(ws), ws.numel(), st))
         check(lib().trex_tree_mf_rows_x3(ptr(M), ptr(S), N, K, nl, N - nl, float(N + 1), 1.0,
                                          ptr(dS), st))
+        # the exact f32 GEMMs (TreeOptimizer(gemm="f32"))
+        check(lib().trex_tree_gram_skip(ptr(S), N, K, nl, ptr(G), ptr(ws), ws.numel(), st))
+        check(lib().trex_tree_mf_rows(ptr(M), ptr(S), N, K, nl, N - nl, ptr(dS), st))
     torch.cuda.synchronize()
     print("ok")
