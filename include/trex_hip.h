@@ -110,7 +110,7 @@ int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
  * Q up to 128 (leaf codes and ancestral states are int8): Q <= 64 on the
  * state-parallel / lane-per-site kernels, 64 < Q <= 128 on the large-alphabet
  * kernel (sankoff_bigq.hip, since ABI v7); Q > 128 returns
- * TREX_E_UNSUPPORTED.  Ragged batches stop at Q = 64.
+ * TREX_E_UNSUPPORTED.  Ragged batches take the same range.
  * ---------------------------------------------------------------------- */
 int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
                      const float* cost, int B, int L, int n_all, int Q, float tau,
@@ -416,9 +416,11 @@ int trex_gumbel_noise(uint64_t seed, const void* state, int64_t n, float* out, v
  * Packed tensors: leaves int8 [sum n_leaves_b L_b] (tree b: [n_leaves_b][L_b]);
  * dp / marginals f32 [sum n_int_b L_b][Q] (tree b: [n_int_b][L_b][Q]);
  * site_score f32 [sum L_b]; anc_states int8 [sum n_int_b L_b];
- * tree_score / d_tree_score [B].  Q <= 64 (Q > 4: the state-parallel
- * kernel, each 64-site item split over ceil(64 / sites-per-wave) waves; its
- * workspace is sized by trex_ragged_workspace_bytes(items, Q)).  phase: 1
+ * tree_score / d_tree_score [B].  Q <= 128 (4 < Q <= 64: the
+ * state-parallel kernel, each 64-site item split over ceil(64 /
+ * sites-per-wave) waves; 64 < Q <= 128: the large-alphabet kernel, a
+ * 128-thread workgroup per item; the workspace is sized by
+ * trex_ragged_workspace_bytes(items, Q)).  phase: 1
  * forward, 2 adjoint, 3 fused (same semantics as trex_sankoff_fwd / _bwd /
  * _fwd_bwd per tree).
  * ---------------------------------------------------------------------- */
