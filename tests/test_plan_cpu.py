@@ -106,6 +106,52 @@ def test_plan_program_reproduces_oracle(kind):
     assert plan.backtrack_ok == (0 if kind == "cycle" else 1)
 
 
+@pytest.mark.parametrize("kind", ["random", "balanced", "fwdref", "dag", "cycle", "unreached"])
+def test_plan_deferred_cherries(kind):
+    """kChildDeferred (bit 28 of a child descriptor) / kStepDeferredIn (flag
+    8, trex_common.h): exactly the cherries (both children leaves or
+    sentinels) with one reached parent are deferred, each by its one parent,
+    and every deferred cherry is stepped before its parent (its adjoint step
+    comes after the parent's, which hands it the parent's cotangent)."""
+    if kind == "random":
+        ch = random_topologies(4, 40, seed=1)
+    elif kind == "balanced":
+        ch = balanced_children(64, B=2)
+    elif kind == "unreached":
+        # 13 becomes an orphan: its cherry 11 has one (unreached) parent,
+        # cherry 10 two parents (14, 13)
+        ch = balanced_children(8).copy()
+        ch[0, 14] = (12, 10)
+    else:
+        ch = weird_children(kind)[None]
+    plan = TreePlan(ch)
+    nl = (ch.shape[1] + 1) // 2
+    ni = ch.shape[1] - nl
+    n_def = 0
+    for b in range(ch.shape[0]):
+        steps = [tuple(int(x) for x in s) for s in plan.fwd_steps[b]]
+        pos = {s[0] & 0xFFFF: k for k, s in enumerate(steps)}
+        flags = {s[0] & 0xFFFF: s[3] for s in steps}
+        kids = {s[0] & 0xFFFF: (s[1], s[2]) for s in steps}
+        parents = {}
+        for s in steps:
+            for d in (s[1], s[2]):
+                if (d >> 24) & 3 == 2:
+                    parents.setdefault(d & 0xFFFF, []).append((s[0] & 0xFFFF, d))
+        for r in range(ni):
+            cherry = all((d >> 24) & 3 != 2 for d in kids[r])
+            ps = parents.get(r, [])
+            want = cherry and len(ps) == 1 and not flags[ps[0][0]] & 2
+            assert bool(flags[r] & 8) == want, (b, r)
+            for p, d in ps:
+                assert bool(d & (1 << 28)) == want
+                if want:
+                    assert pos[r] < pos[p] and not d & (1 << 26)
+            n_def += want
+    if kind in ("random", "balanced"):
+        assert n_def > 0
+
+
 STAGE_WAVES = 8  # kStageWaves (trex_common.h)
 
 
@@ -231,7 +277,7 @@ def test_abi_version_matches_plan_layout():
     the stack depth (include/trex_hip.h); a binding that sized v5 plans
     itself must see the bump.  7 added the device step state (no plan
     change)."""
-    assert lib().trex_version() == 7
+    assert lib().trex_version() == 8
     ch = balanced_children(64, B=1)
     p = TreePlan(ch)
     assert p.n_slots == 5 and p.lane_slots == 12 and p.slot_word == 5 | (13 << 16)

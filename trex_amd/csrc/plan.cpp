@@ -19,6 +19,7 @@
 // This is integer work on B * n_all entries, done once per topology (the
 // reference re-traces per static shape, sankoff.py:114).
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -162,6 +163,18 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
   for (int r = 0; r < ni; ++r) unr += !reach[r];
   *n_unreached = unr;
 
+  // deferred edges (kChildDeferred): cherries with one reached parent
+  // (TREX_DEFER=0 turns them off, A/B)
+  static const bool defer_on = [] {
+    const char* e = std::getenv("TREX_DEFER");
+    return !(e && e[0] == '0');
+  }();
+  std::vector<char> deferred(ni, 0);
+  if (defer_on)
+    for (int c = 0; c < ni; ++c)
+      deferred[c] = refs[c] == 1 && consumer[c] >= 0 && reach[consumer[c]] &&
+                    kids[2 * c].kind != kKindInt && kids[2 * c + 1].kind != kKindInt;
+
   // encode forward steps; set/accumulate flags follow the reverse order
   std::vector<char> seen(ni, 0);
   std::vector<int32_t> enc(4 * ni);
@@ -175,6 +188,7 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
       if (cd.kind == kKindInt) {
         d |= (slot[cd.index] & 0xFF) << 16;
         if (bypass[cd.index]) d |= kChildPrev;
+        if (deferred[cd.index]) d |= kChildDeferred;
         if (reach[r]) {
           if (seen[cd.index]) d |= kStepAccumulate;
           seen[cd.index] = 1;
@@ -186,6 +200,7 @@ bool plan_one_tree(const int32_t* ch, int n_all, int32_t* fwd, int32_t* bt,
     if (r == ni - 1) f |= kStepRoot;
     if (!reach[r]) f |= kStepUnreached;
     if (bypass[r]) f |= kStepToNext;
+    if (deferred[r]) f |= kStepDeferredIn;
     e[3] = f;
   }
   if (order.back() != ni - 1) return false;

@@ -801,7 +801,9 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           const int desc = c == 0 ? s2.y : s2.z;
-          const bool internal = ((desc >> 24) & 3) == kKindInt;
+          // deferred cherries (kChildDeferred) are recomputed, not re-read
+          const bool internal =
+              ((desc >> 24) & 3) == kKindInt && !(desc & kChildDeferred);
           const int vo = internal ? voff : 0x7FFFFFF0;
           const int crow = internal ? (desc & 0xFFFF) : 0;
           bld_row<Q, SPT>(rdp, vo, crow * rowbytes, nd[c]);
@@ -819,6 +821,39 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
             for (int s = 0; s < SPT; ++s) g[i][s] = gnext[i][s];
         } else {
           lds_get<Q, SPT>(slots, (stp.w & kStepRoot) ? kRootSlot : ((stp.x >> 16) & 0xFF), lane, g);
+        }
+        auto leaf_codes = [&](int desc, int kind, int (&code)[SPT]) {
+          if (kind == kKindLeaf) {
+            child_code(desc, code);
+          } else {
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) code[s] = Q;  // all-1e5 row
+          }
+        };
+        if (stp.w & kStepDeferredIn) {
+          // g is the parent's cotangent: this cherry's D is the sum of its two
+          // leaf messages (the forward's order, so bit-identical), then the
+          // parent -> cherry edge adjoint the parent's step skipped
+          float dc[Q][SPT];
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int desc = c == 0 ? stp.y : stp.z;
+            int code[SPT];
+            leaf_codes(desc, (desc >> 24) & 3, code);
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) {
+              float r[Q];
+              lds_vec_get<Q>(tab + code[s] * Q, r);
+#pragma unroll
+              for (int i = 0; i < Q; ++i) dc[i][s] = (c == 0) ? r[i] : dc[i][s] + r[i];
+            }
+          }
+          float gc[Q][SPT];
+          message_adjoint<Q, SPT, MODE>(cf, a, dc, g, acc, gc);
+#pragma unroll
+          for (int i = 0; i < Q; ++i)
+#pragma unroll
+            for (int s = 0; s < SPT; ++s) g[i][s] = gc[i][s];
         }
         if (want_marg) {
           bst_row<Q, SPT>(rmg, voff, row * rowbytes, g);
@@ -843,12 +878,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           if (kind != kKindInt) {
             // leaf / sentinel child: acc_ij += g_i W[code][i][j] (no cotangent)
             int code[SPT];
-            if (kind == kKindLeaf) {
-              child_code(desc, code);
-            } else {
-#pragma unroll
-              for (int s = 0; s < SPT; ++s) code[s] = Q;
-            }
+            leaf_codes(desc, kind, code);
 #pragma unroll
             for (int s = 0; s < SPT; ++s) {
               float w[Q * Q];
@@ -863,7 +893,15 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
             }
           } else {
             float gc[Q][SPT];
-            message_adjoint<Q, SPT, MODE>(cf, a, cd[c], g, acc, gc);
+            if (desc & kChildDeferred) {
+              // the child's step runs this edge (kStepDeferredIn)
+#pragma unroll
+              for (int j = 0; j < Q; ++j)
+#pragma unroll
+                for (int s = 0; s < SPT; ++s) gc[j][s] = g[j][s];
+            } else {
+              message_adjoint<Q, SPT, MODE>(cf, a, cd[c], g, acc, gc);
+            }
             if (desc & kChildPrev) {
 #pragma unroll
               for (int j = 0; j < Q; ++j)
@@ -1385,7 +1423,7 @@ using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 7; }
+extern "C" int trex_version(void) { return 8; }
 
 extern "C" int trex_dp_site_major(int Q) {
   (void)Q;

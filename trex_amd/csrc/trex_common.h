@@ -19,10 +19,18 @@ constexpr int32_t kStepAccumulate = 1 << 26;  // adjoint: add into the slot
 // consumer is this step): forward reads its D from registers, the adjoint
 // hands its cotangent to the next reverse step in registers
 constexpr int32_t kChildPrev = 1 << 27;
+// deferred edge (Q <= 4 adjoint; other kernels ignore it): this internal
+// child is a cherry (both of its children leaves / 1e5 rows) with one
+// parent.  The parent's step hands its own cotangent to the child's slot
+// (or the bypass) instead of the child's, reading no DP row; the child's step
+// (kStepDeferredIn) recomputes its D from its leaf messages and runs the edge
+// adjoint first.  A cherry's row is then never re-read from HBM.
+constexpr int32_t kChildDeferred = 1 << 28;
 // forward-step flags (word 3)
 constexpr int32_t kStepRoot = 1;
 constexpr int32_t kStepUnreached = 2;
 constexpr int32_t kStepToNext = 4;  // output consumed only by the next step (bypass)
+constexpr int32_t kStepDeferredIn = 8;  // slot / bypass holds the parent's cotangent
 
 // Staged (multi-wave) program, after the backtrack entries of a plan: one
 // region of staged_tree_ints(ni) ints per tree, steps [ni][4] (same words as
