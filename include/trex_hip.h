@@ -49,10 +49,9 @@ extern "C" {
 
 const char* trex_last_error(void);
 /* ABI / plan-layout version.
- * 8: trex_tree_mf_adam_seq (the x3 MF with the ancestors' Adam fused in);
- *    plan child descriptors may carry bit 28 and step words flag 8 (deferred
- *    cherry edges of the Q <= 4 adjoint -- plans are passed through
- *    unchanged, so bindings are unaffected).
+ * 8: plan child descriptors may carry bit 28 and step words flag 8 (deferred
+ *    cherry edges of the Q <= 4 adjoint; plans are passed through unchanged,
+ *    so bindings are unaffected).
  * 7: graph-capturable optimiser steps (device step state, *_dev entry
  *    points, trex_gumbel_noise); trex_tree_mf_rows_x3_codes takes the codes
  *    buffer size and Q.
@@ -309,26 +308,6 @@ int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N, int64_t K,
                                void* stream);
 /* (codes_bytes: the size of `codes`, >= trex_tree_leaf_codes_bytes(n_leaf, K / Q);
  * Q must be 4 and K = L * Q -- TREX_E_ARG otherwise, never a silent misread.) */
-/* The MF with the ancestors' Adam + update_seq step fused into it (Q = 4):
- * dS_rows = M[row0 : row0 + nrows] S exactly as trex_tree_mf_rows_x3(_codes)
- * (x3 != 0; codes NULL: the f32 leaf rows) or trex_tree_mf_rows (x3 == 0, no
- * codes), then per (ancestor, site) the step of
- * trex_adam_seq_update_step(_dev) on params / mu / nu [nrows][L][4], and S rows
- * [row0, row0 + nrows) rewritten in place with the next step's softmax --
- * bitwise the same results as the two calls in sequence, without the separate
- * pass over dS.  state non-NULL: bias corrections and temperatures from the
- * device step state (trex_step_advance; count / temperatures ignored), else
- * from count (1-based) and temperature / next_temperature.  Replaces the
- * reference's update_seq VJP + optax adam of the ancestor logits
- * (tests/test_convergence.py:238-261).  TREX_E_UNSUPPORTED (nothing written)
- * for shapes it does not cover: nrows > 256, unaligned buffers, a row block
- * of 2 GiB or more -- the caller then runs the two calls. */
-int trex_tree_mf_adam_seq(const float* M, float* S, int N, int64_t K, int row0, int nrows,
-                          float max_abs_m, float max_abs_s, const void* codes,
-                          int64_t codes_bytes, int n_leaf, int Q, float* dS_rows, float* params,
-                          float* mu, float* nu, float lr, float b1, float b2, float eps,
-                          const void* state, int count, float temperature,
-                          float next_temperature, int x3, void* stream);
 
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */

@@ -630,41 +630,3 @@ def test_tree_optimizer_checkpoint_resume_is_bitwise(device, gemm, tmp_path):
         assert torch.equal(resumed.opt.mu[k], ref.opt.mu[k]) and torch.equal(resumed.opt.nu[k],
                                                                             ref.opt.nu[k]), k
 
-
-@pytest.mark.parametrize("gemm,nl,L,loop", [("x3", 100, 50, False), ("f32", 100, 50, False),
-                                            ("x3", 256, 1001, False), ("f32", 256, 1001, False),
-                                            ("x3", 8, 30, False), ("x3", 16, 52, True),
-                                            ("f32", 16, 52, True), ("x3", 300, 40, False)])
-def test_tree_optimizer_mf_adam_fusion_is_bitwise_neutral(device, monkeypatch, gemm, nl, L, loop):
-    """The ancestors' Adam + update_seq step fused into the MF kernel
-    (trex_tree_mf_adam_seq, the default) == the separate MF + Adam passes
-    (TREX_MF_ADAM=0) bit for bit: losses, parameters, Adam moments and the S
-    rows, over eager steps or the captured device loop; leaf codes (x3, 96
-    code rows + 4 f32 rows at nl = 100), a ragged last column chunk (L =
-    1001), a tiny tree, and n_anc > 256 (no fused kernel: the optimiser falls
-    back by itself)."""
-    params, noise, seqs = _tree_case(nl, L, 4, 29)
-    nz = _t(noise, device)
-    temps = [max(0.1, 2.0 * (1.0 - k / 20)) for k in range(12)]
-    runs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("TREX_MF_ADAM", flag)
-        opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
-                              lr=0.02, gemm=gemm)
-        if loop:
-            opt.step(temps[0], nz, temps[1])
-            lp = opt.device_loop(temps, 77, capture=True)
-            losses = [float(lp.run(1)) for _ in range(4)]
-        else:
-            losses = [float(opt.step(temps[i], nz, temps[i + 1])) for i in range(4)]
-        torch.cuda.synchronize()
-        assert opt.fuse_adam == (flag == "1" and nl <= 257)
-        runs.append((losses, {k: v.clone() for k, v in opt.params.items()},
-                     {k: v.clone() for k, v in opt.opt.mu.items()},
-                     {k: v.clone() for k, v in opt.opt.nu.items()}, opt.S.clone()))
-    a, b = runs
-    assert a[0] == b[0]
-    for i in (1, 2, 3):
-        for k in a[i]:
-            assert torch.equal(a[i][k], b[i][k]), (i, k)
-    assert torch.equal(a[4], b[4])

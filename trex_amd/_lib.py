@@ -93,9 +93,6 @@ SIGNATURES = {
     "trex_tree_leaf_codes": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _c_i64, _p, _p]),
     "trex_tree_mf_rows_x3_codes": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p,
                                           _c_i64, _c_i, _c_i, _p, _p]),
-    "trex_tree_mf_adam_seq": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p, _c_i64,
-                                     _c_i, _c_i, _p, _p, _p, _p, _c_f, _c_f, _c_f, _c_f, _p,
-                                     _c_i, _c_f, _c_f, _c_i, _p]),
     "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),
     "trex_tree_constraint": (_c_i, [_p, _c_i, _c_f, _c_f, _p, _c_i, _p, _p, _p]),
     "trex_tree_compute_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _p, _p, _p]),

@@ -245,7 +245,27 @@ __device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT
 // Site-major DP rows ([row][L][Q]): a lane's SPT consecutive sites x Q states
 // are Q*SPT contiguous floats -> one dwordx4 (Q = 4), dwordx3 or dwordx2
 // access per site.  voff = site*Q*4 (per lane), soff = row*L*Q*4.
-template <int Q, int SPT>
+#ifndef TREX_AUX_FWD
+#define TREX_AUX_FWD 0
+#endif
+#ifndef TREX_AUX_FUSED
+#define TREX_AUX_FUSED 0
+#endif
+#ifndef TREX_AUX_ADJ
+#define TREX_AUX_ADJ 0
+#endif
+#ifndef TREX_AUX_MARG
+#define TREX_AUX_MARG 0
+#endif
+// cache policy of the Q <= 4 kernel's DP-row accesses: forward-only stores,
+// the fused kernel's stores and re-reads, the adjoint-only kernel's reads,
+// marginal stores
+constexpr int kAuxFwdRow = TREX_AUX_FWD, kAuxFusedRow = TREX_AUX_FUSED;
+constexpr int kAuxAdjRow = TREX_AUX_ADJ, kAuxMarg = TREX_AUX_MARG;
+
+// AUX: the buffer instruction's cache-policy bits (2 = nt: a streaming
+// access that should not displace reused lines)
+template <int Q, int SPT, int AUX = 0>
 __device__ __forceinline__ void bst_row(rsrc_t r, int voff, int soff, const float (&d)[Q][SPT]) {
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
@@ -253,31 +273,31 @@ __device__ __forceinline__ void bst_row(rsrc_t r, int voff, int soff, const floa
     if constexpr (Q == 4) {
       u32x4 w = {__float_as_uint(d[0][s]), __float_as_uint(d[1][s]), __float_as_uint(d[2][s]),
                  __float_as_uint(d[3][s])};
-      __builtin_amdgcn_raw_buffer_store_b128(w, r, vo, soff, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(w, r, vo, soff, AUX);
     } else if constexpr (Q == 3) {
       u32x3 w = {__float_as_uint(d[0][s]), __float_as_uint(d[1][s]), __float_as_uint(d[2][s])};
-      __builtin_amdgcn_raw_buffer_store_b96(w, r, vo, soff, 0);
+      __builtin_amdgcn_raw_buffer_store_b96(w, r, vo, soff, AUX);
     } else {
       u32x2 w = {__float_as_uint(d[0][s]), __float_as_uint(d[1][s])};
-      __builtin_amdgcn_raw_buffer_store_b64(w, r, vo, soff, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(w, r, vo, soff, AUX);
     }
   }
 }
 
-template <int Q, int SPT>
+template <int Q, int SPT, int AUX = 0>
 __device__ __forceinline__ void bld_row(rsrc_t r, int voff, int soff, float (&d)[Q][SPT]) {
 #pragma unroll
   for (int s = 0; s < SPT; ++s) {
     const int vo = voff + s * Q * 4;
     if constexpr (Q == 4) {
-      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, 0);
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(r, vo, soff, AUX);
       d[0][s] = __uint_as_float(w.x); d[1][s] = __uint_as_float(w.y);
       d[2][s] = __uint_as_float(w.z); d[3][s] = __uint_as_float(w.w);
     } else if constexpr (Q == 3) {
-      const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(r, vo, soff, 0);
+      const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(r, vo, soff, AUX);
       d[0][s] = __uint_as_float(w.x); d[1][s] = __uint_as_float(w.y); d[2][s] = __uint_as_float(w.z);
     } else {
-      const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, 0);
+      const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, vo, soff, AUX);
       d[0][s] = __uint_as_float(w.x); d[1][s] = __uint_as_float(w.y);
     }
   }
@@ -743,7 +763,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         }
         const int row = stp.x & 0xFFFF;
         const int oslot = (stp.x >> 16) & 0xFF;
-        bst_row<Q, SPT>(rdp, voff, row * rowbytes, dv);
+        bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, voff, row * rowbytes, dv);
         if (!(stp.w & kStepToNext) && oslot != 0xFF) {
           lds_put<Q, SPT>(slots, oslot, lane, dv);
         }
@@ -806,7 +826,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
               ((desc >> 24) & 3) == kKindInt && !(desc & kChildDeferred);
           const int vo = internal ? voff : 0x7FFFFFF0;
           const int crow = internal ? (desc & 0xFFFF) : 0;
-          bld_row<Q, SPT>(rdp, vo, crow * rowbytes, nd[c]);
+          bld_row<Q, SPT, FWD ? kAuxFusedRow : kAuxAdjRow>(rdp, vo, crow * rowbytes, nd[c]);
         }
       };
       float gnext[Q][SPT];  // cotangent handed to the next reverse step (bypass)
@@ -856,7 +876,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
             for (int s = 0; s < SPT; ++s) g[i][s] = gc[i][s];
         }
         if (want_marg) {
-          bst_row<Q, SPT>(rmg, voff, row * rowbytes, g);
+          bst_row<Q, SPT, kAuxMarg>(rmg, voff, row * rowbytes, g);
         }
         if (at && active) {
           int best[SPT];

@@ -839,9 +839,7 @@ __device__ __forceinline__ void softmax4(const float (&x)[4], float T, float (&o
 
 // One ancestor row (Q = 4) of the fused update_seq VJP + Adam + next
 // update_seq: s = softmax(T p) (bitwise the S the step's GEMMs used), g = T s
-// (ds - <s, ds>), Adam on p / m / v, s = softmax(Tn p_new).  Shared by
-// adam_seq_update_kernel and the MF kernel's fused epilogue (mf_kernel5
-// ADAM), so both paths run the same arithmetic.
+// (ds - <s, ds>), Adam on p / m / v, s = softmax(Tn p_new).
 __device__ __forceinline__ void adam_seq_row4(const float (&gv)[4], float (&pv)[4], float (&mv)[4],
                                               float (&vv)[4], float T, float Tn, float lr,
                                               float b1, float b2, float eps, float bc1, float bc2,
@@ -861,17 +859,6 @@ __device__ __forceinline__ void adam_seq_row4(const float (&gv)[4], float (&pv)[
   }
   softmax4(pv, Tn, sv);
 }
-
-// fused ancestors' Adam of the MF kernels (ADAM instantiations): p / mu / nu
-// [nrows][L][4], s = the ancestors' S rows (F + row0 * K), rewritten in place
-struct AdamSeqArgs {
-  float* p;
-  float* mu;
-  float* nu;
-  float* s;
-  float lr, b1, b2, eps, bc1, bc2, T, Tn;
-  const StepState* ss;  // non-null: bc1 / bc2 / T / Tn from the device step state
-};
 
 // b^n by squaring in IEEE double: the host entry points and
 // trex_step_advance compute the same bits (no pow() implementations to
@@ -1129,26 +1116,6 @@ __device__ __forceinline__ h8 tr_pair(const unsigned char* p, int four_rows) {
   return (h8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
 }
 
-// 4 x 4 transpose across a lane quad (DPP quad permutes): lane j of the quad
-// holds v[i] = X[i][j] on entry, v[i] = X[j][i] on exit
-template <int S>  // one butterfly stage: lanes j, j ^ S swap the pairs (i, i + S)
-__device__ __forceinline__ void quad_swap_stage(float (&v)[4], int j) {
-  // quad_perm xor 1 = [1, 0, 3, 2] (0xB1), xor 2 = [2, 3, 0, 1] (0x4E)
-  constexpr int ctrl = S == 1 ? 0xB1 : 0x4E;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (i & S) continue;
-    const float x = (j & S) ? v[i] : v[i + S];
-    const int y = __builtin_amdgcn_update_dpp(0, __float_as_int(x), ctrl, 0xF, 0xF, false);
-    if (j & S) v[i] = __int_as_float(y);
-    else v[i + S] = __int_as_float(y);
-  }
-}
-__device__ __forceinline__ void quad_transpose4(float (&v)[4], int j) {
-  quad_swap_stage<1>(v, j);
-  quad_swap_stage<2>(v, j);
-}
-
 // ---- v3 MF: out = M[row0 : row0 + nrows] F, LDS-staged, persistent --------
 // A workgroup (8 waves, two per SIMD) owns TPC x 32 output columns per chunk
 // and up to 256 output rows (wave w: rows 32w .. 32w + 31 x all TPC column
@@ -1376,23 +1343,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // (one raw item after each column tile), with no branch in the stage body
 // (loads past the split run on neighbouring data or out of bounds: 0, and
 // stage into the buffer nobody reads next).
-//
-// ADAM (Q = 4, nrows <= 256: one workgroup owns every output row of its
-// columns): the ancestors' update_seq VJP + Adam + next update_seq step
-// fused in (AdamSeqArgs, adam_seq_row4).  The chunk epilogue transposes each
-// lane quad's 4 x 4 blocks (DPP quad permutes) so a lane holds whole (row,
-// site) float4s and stores dS as float4s; during the next chunk's stages the
-// lane reloads its own float4s (same lane and address: ordered, L2-hot) with
-// the rows' p / mu / nu, kAdamPer items per stage issued one stage before
-// they are applied, and writes p / mu / nu and the new S row.  A finished
-// chunk's S columns are never read again by this workgroup nor ever by
-// another, so the S rows are rewritten in place; the last chunk's items run
-// after the loop, in batches of 8.
-template <int TPC, bool CODES, bool X3, bool ADAM = false>
+template <int TPC, bool CODES, bool X3>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void mf_kernel5(
-    const float* __restrict__ Mm, const float* F, int N, int K, int row0, int nrows,
+    const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
     int nchunks, float* __restrict__ out, float sm, float sf, const uint8_t* __restrict__ codesR,
-    int lcs, AdamSeqArgs ad) {
+    int lcs) {
   constexpr int CW = TPC * 32;
   constexpr int NIT = 32 * (CW / 4);  // F (row, column group) float4 items per stage
   constexpr int IPT = (NIT + 255) / 256;
@@ -1516,92 +1471,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
   const float unscale = X3 ? 1.0f / (sm * sf) : 1.0f;
 
-  // ---- fused Adam (ADAM): item i of chunk ch, i = u * 4 TPC + 4 t + qg, is
-  // this lane's (row, site) after the quad transpose: row rbase + 32 u +
-  // (lane & 3) + 8 qg + 4 h, columns ch * CW + 32 t + (r & ~3) .. + 3
-  constexpr int kItems = 8 * TPC;
-  constexpr int kAdamPer = 3;  // items per stage (C5: 40 items in 14 of 16 stages)
-  const rsrc_t rp = make_rsrc(ad.p, ADAM ? (uint32_t)((size_t)nrows * K * 4) : 0u);
-  const rsrc_t rmu = make_rsrc(ad.mu, ADAM ? (uint32_t)((size_t)nrows * K * 4) : 0u);
-  const rsrc_t rnu = make_rsrc(ad.nu, ADAM ? (uint32_t)((size_t)nrows * K * 4) : 0u);
-  const rsrc_t rsn = make_rsrc(ad.s, ADAM ? (uint32_t)((size_t)nrows * K * 4) : 0u);
-  float abc1 = ad.bc1, abc2 = ad.bc2, aT = ad.T, aTn = ad.Tn;
-  if (ADAM && ad.ss) {
-    abc1 = ad.ss->bc1;
-    abc2 = ad.ss->bc2;
-    aT = ad.ss->T;
-    aTn = ad.ss->Tn;
-  }
-  auto item_off = [&](int ch, int i) -> int {
-    const int u = i / (4 * TPC), t = (i >> 2) % TPC, qg = i & 3;
-    const int row = rbase + 32 * u + (lane & 3) + 8 * qg + 4 * h;
-    const int col = ch * CW + 32 * t + (r & ~3);
-    return (row < nrows && col < K) ? (row * K + col) * 4 : 0x7FFFFFF0;  // OOB: 0 / dropped
-  };
-  auto adam_load = [&](int o, u32x4 (&d)[4]) {
-    d[0] = __builtin_amdgcn_raw_buffer_load_b128(ro, o, 0, 0);
-    d[1] = __builtin_amdgcn_raw_buffer_load_b128(rp, o, 0, 0);
-    d[2] = __builtin_amdgcn_raw_buffer_load_b128(rmu, o, 0, 0);
-    d[3] = __builtin_amdgcn_raw_buffer_load_b128(rnu, o, 0, 0);
-  };
-  auto adam_apply1 = [&](int o, const u32x4 (&d)[4]) {
-    float g4[4], p4[4], m4[4], v4[4], s4[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      g4[q] = __uint_as_float(d[0][q]);
-      p4[q] = __uint_as_float(d[1][q]);
-      m4[q] = __uint_as_float(d[2][q]);
-      v4[q] = __uint_as_float(d[3][q]);
-    }
-    adam_seq_row4(g4, p4, m4, v4, aT, aTn, ad.lr, ad.b1, ad.b2, ad.eps, abc1, abc2, s4);
-    auto pack = [](const float (&x)[4]) {
-      return (u32x4){__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]),
-                     __float_as_uint(x[3])};
-    };
-    __builtin_amdgcn_raw_buffer_store_b128(pack(p4), rp, o, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(pack(m4), rmu, o, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(pack(v4), rnu, o, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(pack(s4), rsn, o, 0, 0);
-  };
-  int pch = -1, pnext = 0;  // chunk with pending items, its next item to load
-  int pl0 = 0, pload = 0;   // items [pl0, pl0 + pload) loaded, not yet applied
-  u32x4 ald[kAdamPer][4];
-  // one tick per stage: apply the items loaded last stage, load the next ones
-  auto adam_tick = [&]() {
-#pragma unroll
-    for (int u = 0; u < kAdamPer; ++u)
-      if (u < pload) adam_apply1(item_off(pch, pl0 + u), ald[u]);
-    pload = 0;
-    if (pch >= 0 && pnext < kItems) {
-      pl0 = pnext;
-      pload = min(kAdamPer, kItems - pnext);
-#pragma unroll
-      for (int u = 0; u < kAdamPer; ++u)
-        if (u < pload) adam_load(item_off(pch, pl0 + u), ald[u]);
-      pnext += pload;
-    }
-  };
-  // every pending item, loads batched by NB (before a chunk's items replace
-  // them; after the loop)
-  auto adam_flush = [&](auto nb) {
-    constexpr int NB = decltype(nb)::value;
-#pragma unroll
-    for (int u = 0; u < kAdamPer; ++u)
-      if (u < pload) adam_apply1(item_off(pch, pl0 + u), ald[u]);
-    pload = 0;
-    while (pch >= 0 && pnext < kItems) {
-      u32x4 d[NB][4];
-      const int nb_ = min(NB, kItems - pnext);
-#pragma unroll
-      for (int u = 0; u < NB; ++u)
-        if (u < nb_) adam_load(item_off(pch, pnext + u), d[u]);
-#pragma unroll
-      for (int u = 0; u < NB; ++u)
-        if (u < nb_) adam_apply1(item_off(pch, pnext + u), d[u]);
-      pnext += nb_;
-    }
-  };
-
   // cursors: compute (cc, cs); staged stage = compute + 1; loaded = + 2
   int cc = blockIdx.x, cs = 0;
   int sc_ = cs + 1, scc = cc;  // staged-stage cursor
@@ -1622,7 +1491,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const unsigned char* cb = (g & 1) ? buf1 : buf0;
     unsigned char* nb = (g & 1) ? buf0 : buf1;
     const unsigned char* pa = cb + FBUF + (wave * 64 + r) * kMfStride + 16 * h;
-    if constexpr (ADAM) adam_tick();
     int item = 0;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -1670,30 +1538,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (++ls == nst) { ls = 0; lc += gx; }
     if (++sc_ == nst) { sc_ = 0; scc += gx; }
     if (++cs == nst) {  // chunk done: store its tiles, restart the accumulators
-      if constexpr (ADAM) {
-        adam_flush(std::integral_constant<int, kAdamPer>{});
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int t = 0; t < TPC; ++t)
-#pragma unroll
-            for (int qg = 0; qg < 4; ++qg) {
-              float v[4];
-#pragma unroll
-              for (int i = 0; i < 4; ++i) v[i] = acc[u][t][4 * qg + i] * unscale;
-              quad_transpose4(v, lane & 3);
-              __builtin_amdgcn_raw_buffer_store_b128(
-                  (u32x4){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                          __float_as_uint(v[3])},
-                  ro, item_off(cc, u * 4 * TPC + 4 * t + qg), 0, 0);
-            }
-        pch = cc;
-        pnext = 0;
-      }
       // branch-free: columns past K (a ragged last tile) get an out-of-
       // bounds offset, rows past nrows fall outside the store resource
 #pragma unroll
-      for (int u = 0; u < (ADAM ? 0 : 2); ++u) {
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
         for (int t = 0; t < TPC; ++t) {
           const int col = cc * CW + t * 32 + r;
@@ -1716,7 +1564,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     lds_barrier();
   }
-  if constexpr (ADAM) adam_flush(std::integral_constant<int, 8>{});
 }
 
 int cu_count() {
@@ -2025,12 +1872,11 @@ __device__ __forceinline__ void softmaxq(const float* x, int Q, float T, float* 
   for (int q = 0; q < Q; ++q) o[q] = expf(x[q] * T - m) * inv;
 }
 
-template <int QT>
+// any Q <= 32 (a grid-stride loop over rows)
 __global__ __launch_bounds__(256) void adam_seq_update_kernel(
-    const float* __restrict__ ds, int64_t rows, int Qr, float T, float Tn, float* __restrict__ p,
+    const float* __restrict__ ds, int64_t rows, int Q, float T, float Tn, float* __restrict__ p,
     float* __restrict__ mu, float* __restrict__ nu, float lr, float b1, float b2, float eps,
     float bc1, float bc2, float* __restrict__ s_out, const StepState* __restrict__ ss) {
-  const int Q = QT ? QT : Qr;
   if (ss) {
     bc1 = ss->bc1;
     bc2 = ss->bc2;
@@ -2038,57 +1884,85 @@ __global__ __launch_bounds__(256) void adam_seq_update_kernel(
     Tn = ss->Tn;
   }
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < rows; r += (int64_t)gridDim.x * 256) {
-    float pv[QT ? QT : 32], mv[QT ? QT : 32], vv[QT ? QT : 32], gv[QT ? QT : 32],
-        sv[QT ? QT : 32];
-    if constexpr (QT == 4) {
-      const float4 a = reinterpret_cast<const float4*>(p)[r];
-      const float4 d = reinterpret_cast<const float4*>(ds)[r];
-      const float4 m = reinterpret_cast<const float4*>(mu)[r];
-      const float4 v = reinterpret_cast<const float4*>(nu)[r];
-      float p4[4] = {a.x, a.y, a.z, a.w}, g4[4] = {d.x, d.y, d.z, d.w};
-      float m4[4] = {m.x, m.y, m.z, m.w}, v4[4] = {v.x, v.y, v.z, v.w}, s4[4];
-      adam_seq_row4(g4, p4, m4, v4, T, Tn, lr, b1, b2, eps, bc1, bc2, s4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        pv[q] = p4[q];
-        mv[q] = m4[q];
-        vv[q] = v4[q];
-        sv[q] = s4[q];
-      }
-    } else {
-      for (int q = 0; q < Q; ++q) {
-        pv[q] = p[r * Q + q];
-        gv[q] = ds[r * Q + q];
-        mv[q] = mu[r * Q + q];
-        vv[q] = nu[r * Q + q];
-      }
-      softmaxq(pv, Q, T, sv);
-      float dot = sv[0] * gv[0];
-      for (int q = 1; q < Q; ++q) dot = fmaf(sv[q], gv[q], dot);
-      for (int q = 0; q < Q; ++q) {
-        const float gt = T * sv[q] * (gv[q] - dot);
-        const float m = (1.0f - b1) * gt + b1 * mv[q];
-        const float v = (1.0f - b2) * (gt * gt) + b2 * vv[q];
-        mv[q] = m;
-        vv[q] = v;
-        pv[q] = pv[q] + (-lr) * ((m / bc1) / (sqrtf(v / bc2) + eps));
-      }
+    float pv[32], mv[32], vv[32], gv[32], sv[32];
+    for (int q = 0; q < Q; ++q) {
+      pv[q] = p[r * Q + q];
+      gv[q] = ds[r * Q + q];
+      mv[q] = mu[r * Q + q];
+      vv[q] = nu[r * Q + q];
     }
-    if constexpr (QT == 4) {
-      reinterpret_cast<float4*>(p)[r] = make_float4(pv[0], pv[1], pv[2], pv[3]);
-      reinterpret_cast<float4*>(mu)[r] = make_float4(mv[0], mv[1], mv[2], mv[3]);
-      reinterpret_cast<float4*>(nu)[r] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-      reinterpret_cast<float4*>(s_out)[r] = make_float4(sv[0], sv[1], sv[2], sv[3]);
-    } else {
-      softmaxq(pv, Q, Tn, sv);
-      for (int q = 0; q < Q; ++q) {
-        p[r * Q + q] = pv[q];
-        mu[r * Q + q] = mv[q];
-        nu[r * Q + q] = vv[q];
-        s_out[r * Q + q] = sv[q];
-      }
+    softmaxq(pv, Q, T, sv);
+    float dot = sv[0] * gv[0];
+    for (int q = 1; q < Q; ++q) dot = fmaf(sv[q], gv[q], dot);
+    for (int q = 0; q < Q; ++q) {
+      const float gt = T * sv[q] * (gv[q] - dot);
+      const float m = (1.0f - b1) * gt + b1 * mv[q];
+      const float v = (1.0f - b2) * (gt * gt) + b2 * vv[q];
+      mv[q] = m;
+      vv[q] = v;
+      pv[q] = pv[q] + (-lr) * ((m / bc1) / (sqrtf(v / bc2) + eps));
+    }
+    softmaxq(pv, Q, Tn, sv);
+    for (int q = 0; q < Q; ++q) {
+      p[r * Q + q] = pv[q];
+      mu[r * Q + q] = mv[q];
+      nu[r * Q + q] = vv[q];
+      s_out[r * Q + q] = sv[q];
     }
   }
+}
+
+// Q = 4 (16-B rows): one row per thread over a full grid, every stream
+// nontemporal -- 1.63 GB per C5 step touched once, so it should not
+// displace anything in L2 / MALL (C5: 329 -> 272 us, 4.9 -> 6.0 TB/s; two or
+// four rows per thread, or temporal accesses, were slower: DESIGN §9)
+typedef float fv4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void adam_seq_update4_kernel(
+    const fv4* __restrict__ ds, int64_t rows, float T, float Tn, fv4* __restrict__ p,
+    fv4* __restrict__ mu, fv4* __restrict__ nu, float lr, float b1, float b2, float eps,
+    float bc1, float bc2, fv4* __restrict__ s_out, const StepState* __restrict__ ss) {
+  if (ss) {
+    bc1 = ss->bc1;
+    bc2 = ss->bc2;
+    T = ss->T;
+    Tn = ss->Tn;
+  }
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  const fv4 d = __builtin_nontemporal_load(ds + r), a = __builtin_nontemporal_load(p + r);
+  const fv4 m = __builtin_nontemporal_load(mu + r), v = __builtin_nontemporal_load(nu + r);
+  float p4[4], g4[4], m4[4], v4[4], s4[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    p4[q] = a[q];
+    g4[q] = d[q];
+    m4[q] = m[q];
+    v4[q] = v[q];
+  }
+  adam_seq_row4(g4, p4, m4, v4, T, Tn, lr, b1, b2, eps, bc1, bc2, s4);
+  __builtin_nontemporal_store((fv4){p4[0], p4[1], p4[2], p4[3]}, p + r);
+  __builtin_nontemporal_store((fv4){m4[0], m4[1], m4[2], m4[3]}, mu + r);
+  __builtin_nontemporal_store((fv4){v4[0], v4[1], v4[2], v4[3]}, nu + r);
+  __builtin_nontemporal_store((fv4){s4[0], s4[1], s4[2], s4[3]}, s_out + r);
+}
+
+int grid_for(int64_t n, int per = 256, int cap = 8192);
+
+void launch_adam_seq(const float* ds, int64_t rows, int Q, float T, float Tn, float* p, float* mu,
+                     float* nu, float lr, float b1, float b2, float eps, float bc1, float bc2,
+                     float* s_out, const StepState* ss, hipStream_t st) {
+  const bool al = ((reinterpret_cast<uintptr_t>(ds) | reinterpret_cast<uintptr_t>(p) |
+                    reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
+                    reinterpret_cast<uintptr_t>(s_out)) & 15) == 0;
+  if (Q == 4 && al && rows <= 0x7FFFFFFFLL * 256)
+    hipLaunchKernelGGL(adam_seq_update4_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
+                       st, reinterpret_cast<const fv4*>(ds), rows, T, Tn,
+                       reinterpret_cast<fv4*>(p), reinterpret_cast<fv4*>(mu),
+                       reinterpret_cast<fv4*>(nu), lr, b1, b2, eps, bc1, bc2,
+                       reinterpret_cast<fv4*>(s_out), ss);
+  else
+    hipLaunchKernelGGL(adam_seq_update_kernel, dim3(grid_for(rows)), dim3(256), 0, st, ds, rows, Q,
+                       T, Tn, p, mu, nu, lr, b1, b2, eps, bc1, bc2, s_out, ss);
 }
 
 __global__ __launch_bounds__(256) void identity_kernel(int N, float* __restrict__ A) {
@@ -2127,7 +2001,7 @@ __global__ __launch_bounds__(256) void discretize_kernel(const float* __restrict
   for (int j = threadIdx.x; j < n_nodes; j += 256) out[(size_t)i * n_nodes + j] = (j == a) ? 1.0f : 0.0f;
 }
 
-int grid_for(int64_t n, int per = 256, int cap = 8192) {
+int grid_for(int64_t n, int per, int cap) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, cap));
 }
 
@@ -2604,18 +2478,8 @@ extern "C" int trex_adam_seq_update_step(const float* ds_anc, int n_anc, int L, 
   const float bc1 = bias_corr(b1, count);
   const float bc2 = bias_corr(b2, count);
   const int64_t rows = (int64_t)n_anc * L;
-  const bool al = ((reinterpret_cast<uintptr_t>(ds_anc) | reinterpret_cast<uintptr_t>(params) |
-                    reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
-                    reinterpret_cast<uintptr_t>(s_next)) & 15) == 0;
-  hipStream_t st = (hipStream_t)stream;
-  if (Q == 4 && al)
-    hipLaunchKernelGGL(adam_seq_update_kernel<4>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
-                       rows, Q, temperature, next_temperature, params, mu, nu, lr, b1, b2, eps,
-                       bc1, bc2, s_next, (const StepState*)nullptr);
-  else
-    hipLaunchKernelGGL(adam_seq_update_kernel<0>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
-                       rows, Q, temperature, next_temperature, params, mu, nu, lr, b1, b2, eps,
-                       bc1, bc2, s_next, (const StepState*)nullptr);
+  launch_adam_seq(ds_anc, rows, Q, temperature, next_temperature, params, mu, nu, lr, b1, b2, eps,
+                  bc1, bc2, s_next, nullptr, (hipStream_t)stream);
   return tree_hip_check("trex_adam_seq_update_step");
 }
 
@@ -2627,17 +2491,8 @@ extern "C" int trex_adam_seq_update_step_dev(const float* ds_anc, int n_anc, int
       Q > 32)
     return set_error(TREX_E_ARG, "trex_adam_seq_update_step_dev: bad arguments");
   const int64_t rows = (int64_t)n_anc * L;
-  const bool al = ((reinterpret_cast<uintptr_t>(ds_anc) | reinterpret_cast<uintptr_t>(params) |
-                    reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
-                    reinterpret_cast<uintptr_t>(s_next)) & 15) == 0;
-  hipStream_t st = (hipStream_t)stream;
-  const StepState* ss = static_cast<const StepState*>(state);
-  if (Q == 4 && al)
-    hipLaunchKernelGGL(adam_seq_update_kernel<4>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
-                       rows, Q, 1.0f, 1.0f, params, mu, nu, lr, b1, b2, eps, 1.0f, 1.0f, s_next, ss);
-  else
-    hipLaunchKernelGGL(adam_seq_update_kernel<0>, dim3(grid_for(rows)), dim3(256), 0, st, ds_anc,
-                       rows, Q, 1.0f, 1.0f, params, mu, nu, lr, b1, b2, eps, 1.0f, 1.0f, s_next, ss);
+  launch_adam_seq(ds_anc, rows, Q, 1.0f, 1.0f, params, mu, nu, lr, b1, b2, eps, 1.0f, 1.0f, s_next,
+                  static_cast<const StepState*>(state), (hipStream_t)stream);
   return tree_hip_check("trex_adam_seq_update_step_dev");
 }
 
@@ -2717,7 +2572,7 @@ extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N
 namespace {
 int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int row0, int nrows,
           float max_abs_m, float max_abs_s, float* dS_rows, const uint8_t* codesR, int lcs,
-          void* stream, bool x3, const AdamSeqArgs* ad = nullptr);
+          void* stream, bool x3);
 }  // namespace
 extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t K, int row0,
                                  int nrows, float* dS_rows, void* stream) {
@@ -2744,7 +2599,7 @@ namespace {
 // v3 MF launch; codesR / lcs: leaf-code stages (CODES instantiation) or null / 0
 int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int row0, int nrows,
           float max_abs_m, float max_abs_s, float* dS_rows, const uint8_t* codesR, int lcs,
-          void* stream, bool x3, const AdamSeqArgs* ad) {
+          void* stream, bool x3) {
   if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
       row0 + nrows > N || !pos_finite_f32(max_abs_m) || !pos_finite_f32(max_abs_s))
     return set_error(TREX_E_ARG, "%s: bad arguments", fn);
@@ -2784,11 +2639,7 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
   const bool v5_ok = 32LL * K * 4 < 0x7FFFFFF0LL;
   if (!x3 && !v5_ok) return set_error(TREX_E_UNSUPPORTED, "%s: K too large for the f32 v5 MF", fn);
   // f32: v5; x3: v3 (v5 measured 242 vs 224 us with leaf codes at C5) unless TREX_MF=5
-  if (ad && (!v5_ok || rg != 1 || (int64_t)nrows * K * 4 >= 0x7FFFFFF0LL))
-    // the fused Adam (v5 ADAM): one row group (the S rows are rewritten per
-    // chunk by the workgroup that read them), byte offsets below 2^31
-    return set_error(TREX_E_UNSUPPORTED, "%s: no fused Adam for this shape", fn);
-  if (v5_ok && (ad || !x3 || (ev && std::atoi(ev) == 5))) {
+  if (v5_ok && (!x3 || (ev && std::atoi(ev) == 5))) {
     // f32: the transposed F slice is CW x 144 B
     const int lds5 = x3 ? lds : 2 * (160 * kMfStride + 256 * kMfStride);
     auto go5 = [&](auto kernel, int tpc) {
@@ -2798,21 +2649,9 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
       const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
       hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(256), lds5, (hipStream_t)stream, M, S, N,
                          (int)K, row0, nrows, nch, dS_rows, x3 ? split_scale(max_abs_m) : 1.0f,
-                         x3 ? split_scale(max_abs_s) : 1.0f, codesR, lcs,
-                         ad ? *ad : AdamSeqArgs{});
+                         x3 ? split_scale(max_abs_s) : 1.0f, codesR, lcs);
     };
-    if (ad) {
-      if (!x3) {
-        if (best == 5) go5(mf_kernel5<5, false, false, true>, 5);
-        else go5(mf_kernel5<4, false, false, true>, 4);
-      } else if (best == 5) {
-        if (codes) go5(mf_kernel5<5, true, true, true>, 5);
-        else go5(mf_kernel5<5, false, true, true>, 5);
-      } else {
-        if (codes) go5(mf_kernel5<4, true, true, true>, 4);
-        else go5(mf_kernel5<4, false, true, true>, 4);
-      }
-    } else if (!x3) {
+    if (!x3) {
       if (best == 5) go5(mf_kernel5<5, false, false>, 5);
       else go5(mf_kernel5<4, false, false>, 4);
     } else if (best == 5) {
@@ -2905,50 +2744,6 @@ extern "C" int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N,
                                  "trex_tree_leaf_codes_bytes(n_leaf, K / Q)");
   return mf_x3("trex_tree_mf_rows_x3_codes", M, S, N, K, row0, nrows, max_abs_m, max_abs_s,
                dS_rows, static_cast<const uint8_t*>(codes), lcr / 32, stream, true);
-}
-
-extern "C" int trex_tree_mf_adam_seq(const float* M, float* S, int N, int64_t K, int row0,
-                                     int nrows, float max_abs_m, float max_abs_s,
-                                     const void* codes, int64_t codes_bytes, int n_leaf, int Q,
-                                     float* dS_rows, float* params, float* mu, float* nu,
-                                     float lr, float b1, float b2, float eps, const void* state,
-                                     int count, float temperature, float next_temperature,
-                                     int x3, void* stream) {
-  const char* fn = "trex_tree_mf_adam_seq";
-  if (!params || !mu || !nu || Q != 4 || K % 4 != 0 || (!x3 && codes) ||
-      (!state && (count < 1 || !pos_finite_f32(temperature) ||
-                  !pos_finite_f32(next_temperature))))
-    return set_error(TREX_E_ARG, "%s: bad arguments", fn);
-  if (((reinterpret_cast<uintptr_t>(S) | reinterpret_cast<uintptr_t>(dS_rows) |
-        reinterpret_cast<uintptr_t>(params) | reinterpret_cast<uintptr_t>(mu) |
-        reinterpret_cast<uintptr_t>(nu)) & 15) != 0)
-    return set_error(TREX_E_UNSUPPORTED, "%s: buffers must be 16-B aligned", fn);
-  int lcs = 0;
-  if (codes) {
-    const int lcr = trex_tree_leaf_code_rows(n_leaf);
-    if (lcr <= 0 || lcr > N) return set_error(TREX_E_ARG, "%s: bad n_leaf for codes", fn);
-    if (codes_bytes < (int64_t)lcr * (K / Q))
-      return set_error(TREX_E_ARG, "%s: codes buffer too small", fn);
-    lcs = lcr / 32;
-  }
-  AdamSeqArgs ad{};
-  ad.p = params;
-  ad.mu = mu;
-  ad.nu = nu;
-  ad.s = S + (size_t)row0 * K;
-  ad.lr = lr;
-  ad.b1 = b1;
-  ad.b2 = b2;
-  ad.eps = eps;
-  ad.ss = static_cast<const StepState*>(state);
-  if (!state) {
-    ad.bc1 = bias_corr(b1, count);
-    ad.bc2 = bias_corr(b2, count);
-    ad.T = temperature;
-    ad.Tn = next_temperature;
-  }
-  return mf_x3(fn, M, S, N, K, row0, nrows, max_abs_m, max_abs_s, dS_rows,
-               static_cast<const uint8_t*>(codes), lcs, stream, x3 != 0, &ad);
 }
 
 extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,

@@ -23,7 +23,7 @@ import os
 
 import numpy as np
 
-from ._lib import TREX_E_UNSUPPORTED, check, lib, ptr, stream_handle
+from ._lib import check, lib, ptr, stream_handle
 
 
 def _torch():
@@ -442,50 +442,6 @@ class TreeOptimizer:
                                              cb.numel(), ptr(status), stream_handle(dev)))
             if int(status.item()) == 0:
                 self.codes = cb
-        # the ancestors' Adam + update_seq step fused into the MF kernel
-        # (trex_tree_mf_adam_seq: Q = 4, n_anc <= 256, no clipping -- the
-        # clip needs every gradient's norm first); TREX_MF_ADAM=0 keeps the
-        # separate Adam pass (bitwise the same results)
-        self.fuse_adam = (self.Q == 4 and self.n_anc <= 256 and clip_norm is None
-                          and os.environ.get("TREX_MF_ADAM", "1") != "0")
-
-    def _mf(self, st, adam=None):
-        """dS rows of the ancestors = M S (trex_tree_mf_rows[_x3[_codes]]).
-        ``adam`` = (state, count, T, Tn): the ancestors' Adam + update_seq
-        step fused in (trex_tree_mf_adam_seq; state: the device step state
-        pointer or None for count / T / Tn).  Returns whether it was fused."""
-        L_ = lib()
-        N, K = self.N, self.K
-        dS = self.dS[self.n_leaf:]
-        if adam is not None and self.fuse_adam:
-            a = self.opt
-            state, count, T, Tn = adam
-            x3 = self.gemm == "x3"
-            codes = self.codes if x3 else None
-            rc = L_.trex_tree_mf_adam_seq(
-                ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc, float(N + 1), 1.0,
-                ptr(codes) if codes is not None else None,
-                codes.numel() if codes is not None else 0, self.n_leaf, self.Q, ptr(dS),
-                ptr(self.params["ancestors"]), ptr(a.mu["ancestors"]), ptr(a.nu["ancestors"]),
-                float(a.lr), float(a.b1), float(a.b2), float(a.eps), state, int(count),
-                float(T), float(Tn), int(x3), st)
-            if rc == 0:
-                return True
-            if rc != TREX_E_UNSUPPORTED:
-                check(rc)
-            self.fuse_adam = False  # this shape runs the separate pass from now on
-        if self.codes is not None:
-            check(L_.trex_tree_mf_rows_x3_codes(ptr(self.M), ptr(self.S), N, K, self.n_leaf,
-                                                self.n_anc, float(N + 1), 1.0, ptr(self.codes),
-                                                self.codes.numel(), self.n_leaf, self.Q, ptr(dS),
-                                                st))
-        elif self.gemm == "x3":
-            check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
-                                          float(N + 1), 1.0, ptr(dS), st))
-        else:
-            check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
-                                       ptr(dS), st))
-        return False
 
     def step(self, temperature: float, noise, next_temperature=None):
         """One optimisation step; returns the (device) loss before the update.
@@ -520,14 +476,18 @@ class TreeOptimizer:
                                              ptr(self.dA), ptr(self.M), ptr(self.ws), st))
         check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
                                       ptr(self.dA), ptr(self.ws), st))
-        # d loss / dS for the ancestor rows only (leaf rows are fixed data);
-        # without clipping the ancestors' Adam step rides in the MF kernel
-        Tn = T if next_temperature is None else float(next_temperature)
-        fused = False
-        if self.opt.clip is None:
-            fused = self._mf(st, adam=(None, self.opt.count + 1, T, Tn))
+        # d loss / dS for the ancestor rows only (leaf rows are fixed data)
+        if self.codes is not None:
+            check(L_.trex_tree_mf_rows_x3_codes(ptr(self.M), ptr(self.S), N, K, self.n_leaf,
+                                                self.n_anc, float(N + 1), 1.0, ptr(self.codes),
+                                                self.codes.numel(), self.n_leaf, self.Q,
+                                                ptr(self.dS[self.n_leaf:]), st))
+        elif self.gemm == "x3":
+            check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
+                                          float(N + 1), 1.0, ptr(self.dS[self.n_leaf:]), st))
         else:
-            self._mf(st)
+            check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
+                                       ptr(self.dS[self.n_leaf:]), st))
         check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc, 1.0,
                                            ptr(self.grads["tree_params"]), st))
         if self.opt.clip is None:
@@ -545,13 +505,12 @@ class TreeOptimizer:
                                     float(o.b2), float(o.eps), None, 0, 0.0, st))
             # ... and update_seq of the next step folded in (S rows rewritten
             # in place from the new logits)
-            if not fused:
-                check(L_.trex_adam_seq_update_step(ptr(self.dS[self.n_leaf:]), self.n_anc,
-                                                   self.L, self.Q, T, Tn, ptr(p["ancestors"]),
-                                                   ptr(o.mu["ancestors"]),
-                                                   ptr(o.nu["ancestors"]), o.count,
-                                                   float(o.lr), float(o.b1), float(o.b2),
-                                                   float(o.eps), ptr(self.S[self.n_leaf:]), st))
+            Tn = T if next_temperature is None else float(next_temperature)
+            check(L_.trex_adam_seq_update_step(ptr(self.dS[self.n_leaf:]), self.n_anc, self.L,
+                                               self.Q, T, Tn, ptr(p["ancestors"]),
+                                               ptr(o.mu["ancestors"]), ptr(o.nu["ancestors"]),
+                                               o.count, float(o.lr), float(o.b1), float(o.b2),
+                                               float(o.eps), ptr(self.S[self.n_leaf:]), st))
             self._s_temperature = Tn
         else:
             check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]),
@@ -677,19 +636,25 @@ class _TreeDeviceLoop:
         check(L_.trex_tree_constraint_dev(ptr(o.A), N, o.scale, state, ptr(o.loss), 1, ptr(o.dA),
                                           ptr(o.ws), st))
         dS = o.dS[o.n_leaf:]
-        fused = o._mf(st, adam=(state, 0, 1.0, 1.0))
+        if o.codes is not None:
+            check(L_.trex_tree_mf_rows_x3_codes(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc,
+                                                float(N + 1), 1.0, ptr(o.codes), o.codes.numel(),
+                                                o.n_leaf, o.Q, ptr(dS), st))
+        elif o.gemm == "x3":
+            check(L_.trex_tree_mf_rows_x3(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc,
+                                          float(N + 1), 1.0, ptr(dS), st))
+        else:
+            check(L_.trex_tree_mf_rows(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc, ptr(dS), st))
         check(L_.trex_tree_update_tree_bwd(ptr(o.A), ptr(o.dA), None, N, o.n_anc, 1.0,
                                            ptr(o.grads["tree_params"]), st))
         check(L_.trex_adam_step_dev(ptr(p["tree_params"]), ptr(o.grads["tree_params"]),
                                     ptr(a.mu["tree_params"]), ptr(a.nu["tree_params"]),
                                     p["tree_params"].numel(), state, float(a.lr), float(a.b1),
                                     float(a.b2), float(a.eps), None, 0, 0.0, st))
-        if not fused:
-            check(L_.trex_adam_seq_update_step_dev(ptr(dS), o.n_anc, o.L, o.Q, state,
-                                                   ptr(p["ancestors"]), ptr(a.mu["ancestors"]),
-                                                   ptr(a.nu["ancestors"]), float(a.lr),
-                                                   float(a.b1), float(a.b2), float(a.eps),
-                                                   ptr(o.S[o.n_leaf:]), st))
+        check(L_.trex_adam_seq_update_step_dev(ptr(dS), o.n_anc, o.L, o.Q, state,
+                                               ptr(p["ancestors"]), ptr(a.mu["ancestors"]),
+                                               ptr(a.nu["ancestors"]), float(a.lr), float(a.b1),
+                                               float(a.b2), float(a.eps), ptr(o.S[o.n_leaf:]), st))
 
     def run(self, n_steps: int):
         """n_steps steps (graph replays or eager launches); returns the
