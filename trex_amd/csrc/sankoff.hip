@@ -246,20 +246,22 @@ __device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT
 // are Q*SPT contiguous floats -> one dwordx4 (Q = 4), dwordx3 or dwordx2
 // access per site.  voff = site*Q*4 (per lane), soff = row*L*Q*4.
 #ifndef TREX_AUX_FWD
-#define TREX_AUX_FWD 0
+#define TREX_AUX_FWD 2
 #endif
 #ifndef TREX_AUX_FUSED
 #define TREX_AUX_FUSED 0
 #endif
 #ifndef TREX_AUX_ADJ
-#define TREX_AUX_ADJ 0
+#define TREX_AUX_ADJ 2
 #endif
 #ifndef TREX_AUX_MARG
-#define TREX_AUX_MARG 0
+#define TREX_AUX_MARG 2
 #endif
-// cache policy of the Q <= 4 kernel's DP-row accesses: forward-only stores,
-// the fused kernel's stores and re-reads, the adjoint-only kernel's reads,
-// marginal stores
+// cache policy of the Q <= 4 kernel's DP-row accesses (2 = nt): the
+// forward-only kernel's row stores and the adjoint-only kernel's row reads
+// and marginal stores stream (C4 forward 620 -> 560 us, adjoint 588 -> ~577
+// us); the fused kernel re-reads its rows within the same wave's life, from
+// L2 / MALL in part, so its accesses stay temporal
 constexpr int kAuxFwdRow = TREX_AUX_FWD, kAuxFusedRow = TREX_AUX_FUSED;
 constexpr int kAuxAdjRow = TREX_AUX_ADJ, kAuxMarg = TREX_AUX_MARG;
 
@@ -528,6 +530,9 @@ constexpr int kWTab = 32;  // (Q + 1) Q <= 20 message floats precede the weights
 #endif
 #ifndef TREX_ADJ_WPE
 #define TREX_ADJ_WPE 5
+#endif
+#ifndef TREX_FUSED_WPE
+#define TREX_FUSED_WPE TREX_ADJ_WPE
 #endif
 #ifndef TREX_FWD_WPE
 #define TREX_FWD_WPE 6
@@ -1001,7 +1006,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 }
 
 template <int Q, int SPT, bool SOFT, int PHASE, bool RAGGED = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? TREX_FWD_WPE : TREX_ADJ_WPE, 8)))
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? TREX_FWD_WPE : PHASE == 2 ? TREX_ADJ_WPE : TREX_FUSED_WPE, 8)))
 void sankoff_kernel(KArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if constexpr (!SOFT) {
