@@ -534,6 +534,9 @@ constexpr int kWTab = 32;  // (Q + 1) Q <= 20 message floats precede the weights
 #ifndef TREX_FUSED_WPE
 #define TREX_FUSED_WPE TREX_ADJ_WPE
 #endif
+#ifndef TREX_FUSED_WPE_MAX
+#define TREX_FUSED_WPE_MAX 8
+#endif
 #ifndef TREX_FWD_WPE
 #define TREX_FWD_WPE 6
 #endif
@@ -1006,7 +1009,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 }
 
 template <int Q, int SPT, bool SOFT, int PHASE, bool RAGGED = false>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? TREX_FWD_WPE : PHASE == 2 ? TREX_ADJ_WPE : TREX_FUSED_WPE, 8)))
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PHASE == 1 ? TREX_FWD_WPE : PHASE == 2 ? TREX_ADJ_WPE : TREX_FUSED_WPE, PHASE == 3 ? TREX_FUSED_WPE_MAX : 8)))
 void sankoff_kernel(KArgs A) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if constexpr (!SOFT) {
