@@ -309,6 +309,22 @@ int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N, int64_t K,
 /* (codes_bytes: the size of `codes`, >= trex_tree_leaf_codes_bytes(n_leaf, K / Q);
  * Q must be 4 and K = L * Q -- TREX_E_ARG otherwise, never a silent misread.) */
 
+/* One C5 step's middle and tail in fewer launches (bitwise the separate
+ * calls): trex_tree_surrogate_constraint = trex_tree_surrogate_combine then
+ * trex_tree_constraint[_dev] with accumulate = 1 (state non-NULL: grad_scale
+ * from the device step state's temperature; workspace holds N + (N-1)/2
+ * doubles of partials); trex_tree_update_tree_bwd_adam =
+ * trex_tree_update_tree_bwd then trex_adam_step[_dev] on the tree_params
+ * (no clipping; dtheta may be NULL; state non-NULL: bias corrections from it,
+ * count ignored).  tree.py:133-160 / 50-107 and optax adam. */
+int trex_tree_surrogate_constraint(const float* A, const float* G, int N, float scale,
+                                   float grad_scale, const void* state, float* loss, float* dA,
+                                   float* M, void* workspace, void* stream);
+int trex_tree_update_tree_bwd_adam(const float* A, const float* dA, const float* gates, int N,
+                                   int n_anc, float T, float* dtheta, float* params, float* mu,
+                                   float* nu, int count, const void* state, float lr, float b1,
+                                   float b2, float eps, void* stream);
+
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */
 int trex_tree_soft_cost(const float* S, const float* A, const float* C, int ckind, int N, int L,

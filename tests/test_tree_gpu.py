@@ -630,3 +630,96 @@ def test_tree_optimizer_checkpoint_resume_is_bitwise(device, gemm, tmp_path):
         assert torch.equal(resumed.opt.mu[k], ref.opt.mu[k]) and torch.equal(resumed.opt.nu[k],
                                                                             ref.opt.nu[k]), k
 
+
+
+@pytest.mark.parametrize("dev_state", [False, True])
+def test_fused_step_entries_are_bitwise_separate(device, dev_state):
+    """trex_tree_surrogate_constraint == trex_tree_surrogate_combine +
+    trex_tree_constraint[_dev] (accumulate), and trex_tree_update_tree_bwd_adam
+    == trex_tree_update_tree_bwd + trex_adam_step[_dev], bit for bit (loss,
+    dA, M; gradient, params, moments), with host or device-state counts."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    nl = 40
+    N, na = 2 * nl - 1, nl - 1
+    g = torch.Generator(device=device).manual_seed(3)
+    A = torch.softmax(torch.randn((N, N), device=device, generator=g) * 2, dim=1).contiguous()
+    Gm = torch.rand((N, N), device=device, generator=g) * 100
+    Gm = (Gm + Gm.T).contiguous()
+    dA0 = torch.randn((N, N), device=device, generator=g)
+    th0 = torch.randn((N - 1, na), device=device, generator=g)
+    mu0 = torch.randn((N - 1, na), device=device, generator=g) * 1e-2
+    nu0 = torch.rand((N - 1, na), device=device, generator=g) * 1e-3
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=device)
+    st = stream_handle(device)
+    T, count, scale = 0.7, 4, 10.0
+    state = s_ptr = None
+    if dev_state:
+        state = torch.zeros(8, dtype=torch.int32, device=device)
+        state[0] = count - 1
+        check(lib().trex_step_advance(ptr(state), 0.9, 0.999, ptr(torch.tensor([T] * 8, device=device)),
+                                      8, st))
+        s_ptr = ptr(state)
+    out = []
+    for fused in (False, True):
+        loss = torch.zeros(1, device=device)
+        dA = torch.empty_like(dA0)
+        M = torch.empty_like(dA0)
+        if fused:
+            check(lib().trex_tree_surrogate_constraint(ptr(A), ptr(Gm), N, scale, T, s_ptr,
+                                                       ptr(loss), ptr(dA), ptr(M), ptr(ws), st))
+        else:
+            check(lib().trex_tree_surrogate_combine(ptr(A), ptr(Gm), N, ptr(loss), ptr(dA), ptr(M),
+                                                    ptr(ws), st))
+            if dev_state:
+                check(lib().trex_tree_constraint_dev(ptr(A), N, scale, s_ptr, ptr(loss), 1,
+                                                     ptr(dA), ptr(ws), st))
+            else:
+                check(lib().trex_tree_constraint(ptr(A), N, scale, T, ptr(loss), 1, ptr(dA),
+                                                 ptr(ws), st))
+        th, mu, nu = th0.clone(), mu0.clone(), nu0.clone()
+        gr = torch.empty_like(th0)
+        if fused:
+            check(lib().trex_tree_update_tree_bwd_adam(ptr(A), ptr(dA0), None, N, na, 1.3, ptr(gr),
+                                                       ptr(th), ptr(mu), ptr(nu), count, s_ptr,
+                                                       0.01, 0.9, 0.999, 1e-8, st))
+        else:
+            check(lib().trex_tree_update_tree_bwd(ptr(A), ptr(dA0), None, N, na, 1.3, ptr(gr), st))
+            if dev_state:
+                check(lib().trex_adam_step_dev(ptr(th), ptr(gr), ptr(mu), ptr(nu), th.numel(),
+                                               s_ptr, 0.01, 0.9, 0.999, 1e-8, None, 0, 0.0, st))
+            else:
+                check(lib().trex_adam_step(ptr(th), ptr(gr), ptr(mu), ptr(nu), th.numel(), count,
+                                           0.01, 0.9, 0.999, 1e-8, None, 0, 0.0, st))
+        torch.cuda.synchronize()
+        out.append((loss, dA, M, gr, th, mu, nu))
+    for a, b, name in zip(out[0], out[1], ("loss", "dA", "M", "grad", "params", "mu", "nu")):
+        assert torch.equal(a, b), name
+
+
+def test_tree_device_loop_after_more_eager_steps(device):
+    """A captured device loop, then eager steps (which count on the host
+    only), then the same loop again: bitwise the all-eager run (the loop
+    re-syncs the device step record in place before replaying)."""
+    params, _, seqs = _tree_case(16, 52, 4, 31)
+    temps = [max(0.1, 2.0 * (1.0 - k / 50)) for k in range(14)]
+    seed = 99
+    ref = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                          lr=0.01)
+    dut = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                          lr=0.01)
+    shape = (ref.N - 1, ref.n_anc)
+
+    def eager(o, k):
+        return float(o.step(temps[k - 1], G.gumbel_noise_step(seed, k, shape, device), temps[k]))
+
+    loop = dut.device_loop(temps, seed, capture=True)
+    for k in range(1, 4):
+        assert float(loop.run(1)) == eager(ref, k), k
+    for k in range(4, 6):
+        assert eager(dut, k) == eager(ref, k), k
+    for k in range(6, 9):
+        assert float(loop.run(1)) == eager(ref, k), k
+    torch.cuda.synchronize()
+    for k in ref.params:
+        assert torch.equal(dut.params[k], ref.params[k]), k

@@ -1737,6 +1737,66 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
   }
 }
 
+// update_tree's VJP (update_tree_bwd_kernel's arithmetic) with the
+// tree_params' Adam step (adam_kernel's, no clip) applied in the same pass:
+// one block per row, the gradient optionally written out as well
+__global__ __launch_bounds__(256) void update_tree_bwd_adam_kernel(
+    const float* __restrict__ A, const float* __restrict__ dA, const float* __restrict__ gates,
+    int N, int n_anc, float T, float* __restrict__ dtheta, float* __restrict__ p,
+    float* __restrict__ mu, float* __restrict__ nu, float lr, float b1, float b2, float eps,
+    float bc1, float bc2, const StepState* __restrict__ ss) {
+  __shared__ double sh[256];
+  if (ss) {
+    bc1 = ss->bc1;
+    bc2 = ss->bc2;
+  }
+  const int i = blockIdx.x;  // rows 0..N-2
+  const int nl = N - n_anc;
+  double dot = 0.0;
+  for (int j = threadIdx.x; j < N; j += 256)
+    dot += (double)A[(size_t)i * N + j] * (double)dA[(size_t)i * N + j];
+  const float d = (float)block_sum_256(dot, sh);
+  for (int ja = threadIdx.x; ja < n_anc; ja += 256) {
+    const int j = nl + ja;
+    const bool valid = (i < nl) || (ja > i - nl);
+    float g = 0.0f;
+    if (valid) {
+      const float a = A[(size_t)i * N + j];
+      g = a * (dA[(size_t)i * N + j] - d) / T;
+      if (gates) g *= gates[(size_t)i * n_anc + ja];
+    }
+    const size_t t = (size_t)i * n_anc + ja;
+    if (dtheta) dtheta[t] = g;
+    const float m = (1.0f - b1) * g + b1 * mu[t];
+    const float v = (1.0f - b2) * (g * g) + b2 * nu[t];
+    mu[t] = m;
+    nu[t] = v;
+    const float mh = m / bc1;
+    const float vh = v / bc2;
+    p[t] = p[t] + (-lr) * (mh / (sqrtf(vh) + eps));
+  }
+}
+
+// loss = rows (x 1) then + cols x gscale: the two sum_rows_kernel launches of
+// trex_tree_surrogate_combine + trex_tree_constraint in one, same arithmetic
+__global__ __launch_bounds__(256) void sum_rows2_kernel(const double* __restrict__ v1, int n1,
+                                                       const double* __restrict__ v2, int n2,
+                                                       float scale2, float* __restrict__ out,
+                                                       const StepState* __restrict__ ss) {
+  __shared__ double sh[256];
+  if (ss) scale2 = ss->T;
+  double s = 0.0;
+  for (int t = threadIdx.x; t < n1; t += 256) s += v1[t];
+  s = block_sum_256(s, sh);
+  double s2 = 0.0;
+  for (int t = threadIdx.x; t < n2; t += 256) s2 += v2[t];
+  s2 = block_sum_256(s2, sh);
+  if (threadIdx.x == 0) {
+    const float first = 0.0f + (float)(s * 1.0f);
+    out[0] = first + (float)(s2 * scale2);
+  }
+}
+
 // optax transformations of src/trex/evals/benchmark.py:41-72
 // (create_optimizer), optionally after clip_by_global_norm:
 //   kind 0 adam(lr, b1, b2, eps)        s1 = mu, s2 = nu (bias-corrected)
@@ -2402,6 +2462,22 @@ extern "C" int trex_step_advance(void* state, float b1, float b2, const float* t
   return tree_hip_check("trex_step_advance");
 }
 
+extern "C" int trex_tree_update_tree_bwd_adam(const float* A, const float* dA, const float* gates,
+                                              int N, int n_anc, float T, float* dtheta,
+                                              float* params, float* mu, float* nu, int count,
+                                              const void* state, float lr, float b1, float b2,
+                                              float eps, void* stream) {
+  if (!A || !dA || !params || !mu || !nu || N < 2 || n_anc <= 0 || n_anc >= N ||
+      !pos_finite_f32(T) || (!state && count < 1))
+    return set_error(TREX_E_ARG, "trex_tree_update_tree_bwd_adam: bad arguments");
+  const float bc1 = state ? 1.0f : bias_corr(b1, count);
+  const float bc2 = state ? 1.0f : bias_corr(b2, count);
+  hipLaunchKernelGGL(update_tree_bwd_adam_kernel, dim3(N - 1), dim3(256), 0, (hipStream_t)stream,
+                     A, dA, gates, N, n_anc, T, dtheta, params, mu, nu, lr, b1, b2, eps, bc1, bc2,
+                     static_cast<const StepState*>(state));
+  return tree_hip_check("trex_tree_update_tree_bwd_adam");
+}
+
 extern "C" int trex_adam_step_dev(float* params, const float* grads, float* mu, float* nu,
                                   int64_t n, const void* state, float lr, float b1, float b2,
                                   float eps, const double* grad_sq_norm_parts, int n_parts,
@@ -2554,6 +2630,26 @@ extern "C" int trex_tree_gram_mirror(float* G, int N, int row0, void* stream) {
 extern "C" int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* workspace,
                               int64_t workspace_bytes, void* stream) {
   return trex_tree_gram_skip(S, N, K, 0, G, workspace, workspace_bytes, stream);
+}
+
+extern "C" int trex_tree_surrogate_constraint(const float* A, const float* G, int N, float scale,
+                                              float grad_scale, const void* state, float* loss,
+                                              float* dA, float* M, void* workspace,
+                                              void* stream) {
+  if (!A || !G || !loss || !dA || !M || !workspace || N < 3)
+    return set_error(TREX_E_ARG, "trex_tree_surrogate_constraint: bad arguments");
+  const int n_anc = (N - 1) / 2;
+  hipStream_t st = (hipStream_t)stream;
+  double* rowloss = static_cast<double*>(workspace);
+  double* colloss = rowloss + N;
+  const StepState* ss = static_cast<const StepState*>(state);
+  hipLaunchKernelGGL(surrogate_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, dA, M,
+                     rowloss);
+  hipLaunchKernelGGL(constraint_kernel, dim3(n_anc), dim3(256), 0, st, A, N, scale, grad_scale,
+                     colloss, dA, ss);
+  hipLaunchKernelGGL(sum_rows2_kernel, dim3(1), dim3(256), 0, st, rowloss, N, colloss, n_anc,
+                     grad_scale, loss, ss);
+  return tree_hip_check("trex_tree_surrogate_constraint");
 }
 
 extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N, float* loss,

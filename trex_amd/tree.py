@@ -296,6 +296,18 @@ class Adam:
         # a kernel each step), so a step captured in a hipGraph replays with
         # the right count (trex_step_advance; bitwise the host-count update)
         self.state = step_state(dev)
+        # TreeOptimizer's eager step counts on the host only (no launch);
+        # sync_state() brings the device record up to date before any
+        # device-side use
+        self._state_stale = False
+
+    def sync_state(self):
+        """Reset the device step record to the host count, in place (a
+        captured graph keeps its pointer), when eager steps left it behind."""
+        if self._state_stale:
+            self.state.zero_()
+            self.state[0] = int(self.count)
+            self._state_stale = False
 
     def state_dict(self) -> dict:
         """Host copies of the optimiser state: step count, first / second
@@ -314,11 +326,13 @@ class Adam:
                     raise ValueError(f"Adam.load_state_dict: {name}[{k!r}] does not match")
                 mine[k].copy_(v.to(mine[k].device, dtype=mine[k].dtype))
         self.count = int(sd["count"])
-        self.state = step_state(self.state.device, self.count)
+        self._state_stale = True
+        self.sync_state()
 
     def step(self, params: dict, grads: dict):
         """One update; launches only kernels (graph-capturable unless the
         clip norm is all-reduced over a process group)."""
+        self.sync_state()
         self.count += 1
         st = stream_handle(next(iter(params.values())).device)
         check(lib().trex_step_advance(ptr(self.state), float(self.b1), float(self.b2), None, 0,
@@ -472,10 +486,11 @@ class TreeOptimizer:
         if self.reducer is not None:
             self.reducer(self.G[self.g_row0:])
             check(L_.trex_tree_gram_mirror(ptr(self.G), N, self.g_row0, st))
-        check(L_.trex_tree_surrogate_combine(ptr(self.A), ptr(self.G), N, ptr(self.loss),
-                                             ptr(self.dA), ptr(self.M), ptr(self.ws), st))
-        check(L_.trex_tree_constraint(ptr(self.A), N, self.scale, T, ptr(self.loss), 1,
-                                      ptr(self.dA), ptr(self.ws), st))
+        # surrogate loss / dA / M, then the graph constraint (loss and dA
+        # accumulated), one reduce for both
+        check(L_.trex_tree_surrogate_constraint(ptr(self.A), ptr(self.G), N, self.scale, T, None,
+                                                ptr(self.loss), ptr(self.dA), ptr(self.M),
+                                                ptr(self.ws), st))
         # d loss / dS for the ancestor rows only (leaf rows are fixed data)
         if self.codes is not None:
             check(L_.trex_tree_mf_rows_x3_codes(ptr(self.M), ptr(self.S), N, K, self.n_leaf,
@@ -488,21 +503,20 @@ class TreeOptimizer:
         else:
             check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
                                        ptr(self.dS[self.n_leaf:]), st))
-        check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc, 1.0,
-                                           ptr(self.grads["tree_params"]), st))
         if self.opt.clip is None:
+            o = self.opt
+            o.count += 1
+            # the device step record catches up lazily (Adam.sync_state)
+            o._state_stale = True
+            # update_tree's VJP with the tree_params' Adam step in one pass
+            check(L_.trex_tree_update_tree_bwd_adam(
+                ptr(self.A), ptr(self.dA), None, N, self.n_anc, 1.0,
+                ptr(self.grads["tree_params"]), ptr(p["tree_params"]),
+                ptr(o.mu["tree_params"]), ptr(o.nu["tree_params"]), o.count, None,
+                float(o.lr), float(o.b1), float(o.b2), float(o.eps), st))
             # update_seq VJP fused into the ancestors' Adam update (the logits
             # gradient never round-trips through HBM); bitwise the same as
             # update_seq_bwd + Adam.step
-            o = self.opt
-            o.count += 1
-            # keep the device step state in step with the host count (a
-            # later device_loop continues from it)
-            check(L_.trex_step_advance(ptr(o.state), float(o.b1), float(o.b2), None, 0, st))
-            check(L_.trex_adam_step(ptr(p["tree_params"]), ptr(self.grads["tree_params"]),
-                                    ptr(o.mu["tree_params"]), ptr(o.nu["tree_params"]),
-                                    p["tree_params"].numel(), o.count, float(o.lr), float(o.b1),
-                                    float(o.b2), float(o.eps), None, 0, 0.0, st))
             # ... and update_seq of the next step folded in (S rows rewritten
             # in place from the new logits)
             Tn = T if next_temperature is None else float(next_temperature)
@@ -513,6 +527,8 @@ class TreeOptimizer:
                                                float(o.eps), ptr(self.S[self.n_leaf:]), st))
             self._s_temperature = Tn
         else:
+            check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc,
+                                               1.0, ptr(self.grads["tree_params"]), st))
             check(L_.trex_tree_update_seq_bwd(ptr(self.S[self.n_leaf:]),
                                               ptr(self.dS[self.n_leaf:]), self.n_anc, self.L,
                                               self.Q, T, ptr(self.grads["ancestors"]), st))
@@ -596,6 +612,7 @@ class _TreeDeviceLoop:
         self.seed = int(noise_seed) & (2**64 - 1)
         self.noise = torch.empty((opt.N - 1, opt.n_anc), dtype=torch.float32, device=dev)
         self.graph = None
+        opt.opt.sync_state()
         k0 = opt.opt.count  # steps taken so far
         if k0 >= self.n_temps:
             raise ValueError("temperatures must cover the next step")
@@ -631,10 +648,8 @@ class _TreeDeviceLoop:
         else:
             check(L_.trex_tree_gram_skip(ptr(o.S), N, K, o.skip_rows, ptr(o.G), ptr(o.ws),
                                          o.ws.numel(), st))
-        check(L_.trex_tree_surrogate_combine(ptr(o.A), ptr(o.G), N, ptr(o.loss), ptr(o.dA),
-                                             ptr(o.M), ptr(o.ws), st))
-        check(L_.trex_tree_constraint_dev(ptr(o.A), N, o.scale, state, ptr(o.loss), 1, ptr(o.dA),
-                                          ptr(o.ws), st))
+        check(L_.trex_tree_surrogate_constraint(ptr(o.A), ptr(o.G), N, o.scale, 0.0, state,
+                                                ptr(o.loss), ptr(o.dA), ptr(o.M), ptr(o.ws), st))
         dS = o.dS[o.n_leaf:]
         if o.codes is not None:
             check(L_.trex_tree_mf_rows_x3_codes(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc,
@@ -645,12 +660,10 @@ class _TreeDeviceLoop:
                                           float(N + 1), 1.0, ptr(dS), st))
         else:
             check(L_.trex_tree_mf_rows(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc, ptr(dS), st))
-        check(L_.trex_tree_update_tree_bwd(ptr(o.A), ptr(o.dA), None, N, o.n_anc, 1.0,
-                                           ptr(o.grads["tree_params"]), st))
-        check(L_.trex_adam_step_dev(ptr(p["tree_params"]), ptr(o.grads["tree_params"]),
-                                    ptr(a.mu["tree_params"]), ptr(a.nu["tree_params"]),
-                                    p["tree_params"].numel(), state, float(a.lr), float(a.b1),
-                                    float(a.b2), float(a.eps), None, 0, 0.0, st))
+        check(L_.trex_tree_update_tree_bwd_adam(
+            ptr(o.A), ptr(o.dA), None, N, o.n_anc, 1.0, ptr(o.grads["tree_params"]),
+            ptr(p["tree_params"]), ptr(a.mu["tree_params"]), ptr(a.nu["tree_params"]), 0, state,
+            float(a.lr), float(a.b1), float(a.b2), float(a.eps), st))
         check(L_.trex_adam_seq_update_step_dev(ptr(dS), o.n_anc, o.L, o.Q, state,
                                                ptr(p["ancestors"]), ptr(a.mu["ancestors"]),
                                                ptr(a.nu["ancestors"]), float(a.lr), float(a.b1),
@@ -662,6 +675,7 @@ class _TreeDeviceLoop:
         o = self.opt
         if o.opt.count + n_steps > self.n_temps:
             raise ValueError("the temperature schedule does not cover these steps")
+        o.opt.sync_state()  # eager steps since the capture counted on the host
         for _ in range(int(n_steps)):
             if self.graph is not None:
                 self.graph.replay()
