@@ -51,7 +51,8 @@ const char* trex_last_error(void);
 /* ABI / plan-layout version.
  * 8: plan child descriptors may carry bit 28 and step words flag 8 (deferred
  *    cherry edges of the Q <= 4 adjoint; plans are passed through unchanged,
- *    so bindings are unaffected).
+ *    so bindings are unaffected); trex_tree_surrogate_constraint and
+ *    trex_tree_update_tree_bwd_adam (fewer launches per C5 step).
  * 7: graph-capturable optimiser steps (device step state, *_dev entry
  *    points, trex_gumbel_noise); trex_tree_mf_rows_x3_codes takes the codes
  *    buffer size and Q.
