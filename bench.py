@@ -422,28 +422,16 @@ def c5_gemm_kernels(torch, opt):
     """HIP-event time of the step's two GEMM launches on the optimiser's own
     buffers, with their algorithmic HBM bytes and (f16x3) the MFMA flops the
     tile plan issues -- executed work, not a trex-equivalent rate."""
-    from trex_amd._lib import check, lib, ptr, stream_handle
+    from trex_amd._lib import lib, stream_handle
 
     L_ = lib()
     st = stream_handle(opt.S.device)
     cs = torch.cuda.current_stream(opt.S.device)
     N, K, nl, na = opt.N, opt.K, opt.n_leaf, opt.n_anc
-    dS = opt.dS[nl:]
-    if opt.gemm == "x3":
-        gram = lambda: check(L_.trex_tree_gram_skip_x3(ptr(opt.S), N, K, opt.skip_rows, 1.0,  # noqa: E731
-                                                       ptr(opt.G), ptr(opt.ws), opt.ws.numel(), st))
-        if opt.codes is not None:  # the step's own MF: leaf rows read as codes
-            mf = lambda: check(L_.trex_tree_mf_rows_x3_codes(  # noqa: E731
-                ptr(opt.M), ptr(opt.S), N, K, nl, na, float(N + 1), 1.0, ptr(opt.codes),
-                opt.codes.numel(), nl, opt.Q, ptr(dS), st))
-        else:
-            mf = lambda: check(L_.trex_tree_mf_rows_x3(ptr(opt.M), ptr(opt.S), N, K, nl, na,  # noqa: E731
-                                                       float(N + 1), 1.0, ptr(dS), st))
-    else:
-        gram = lambda: check(L_.trex_tree_gram_skip(ptr(opt.S), N, K, opt.skip_rows, ptr(opt.G),  # noqa: E731
-                                                    ptr(opt.ws), opt.ws.numel(), st))
-        mf = lambda: check(L_.trex_tree_mf_rows(ptr(opt.M), ptr(opt.S), N, K, nl, na, ptr(dS),  # noqa: E731
-                                                st))
+    # the step's own GEMM launches (pre-split operands on the x3 path, leaf
+    # rows read as codes where the optimiser does)
+    gram = lambda: opt._gram(st)  # noqa: E731
+    mf = lambda: opt._mf(st)  # noqa: E731
 
     def timed(fn, reps=20):
         fn()

@@ -317,14 +317,43 @@ int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N, int64_t K,
  * doubles of partials); trex_tree_update_tree_bwd_adam =
  * trex_tree_update_tree_bwd then trex_adam_step[_dev] on the tree_params
  * (no clipping; dtheta may be NULL; state non-NULL: bias corrections from it,
- * count ignored).  tree.py:133-160 / 50-107 and optax adam. */
+ * count ignored).  tree.py:133-160 / 50-107 and optax adam.  M16 (optional):
+ * M also written pre-split for trex_tree_mf_rows_x3p (below), ldm16 >= N
+ * f32-equivalent columns per row, zero past N. */
 int trex_tree_surrogate_constraint(const float* A, const float* G, int N, float scale,
                                    float grad_scale, const void* state, float* loss, float* dA,
-                                   float* M, void* workspace, void* stream);
+                                   float* M, float max_abs_m, void* M16, int ldm16,
+                                   void* workspace, void* stream);
 int trex_tree_update_tree_bwd_adam(const float* A, const float* dA, const float* gates, int N,
                                    int n_anc, float T, float* dtheta, float* params, float* mu,
                                    float* nu, int count, const void* state, float lr, float b1,
                                    float b2, float eps, void* stream);
+
+/* Pre-split f16x3 operands ("x3p").  The x3 GEMMs split every f32 operand
+ * x * s (s = 2^(14 - ceil(log2 max_abs))) into f16 hi + lo each time they
+ * stage it.  trex_tree_split_x3 stores that split once: every group of 4
+ * consecutive values becomes 16 bytes (4 f16 hi, then 4 f16 lo), rows of ldo
+ * f32-equivalent columns (ldo % 4 == 0, groups past cols zero), so the
+ * pre-split operand has the f32 operand's byte offsets.  The x3p GEMMs read
+ * it without the split arithmetic and give bitwise the x3 results:
+ * trex_tree_gram_skip_x3p(S16, ...) == trex_tree_gram_skip_x3(S, ...);
+ * trex_tree_mf_rows_x3p(M16, ldm, S16, ...) == trex_tree_mf_rows_x3[_codes]
+ * (M16 rows ldm apart, ldm % 32 == 0, zero past N; codes optional);
+ * trex_adam_seq_update_step_x3p == trex_adam_seq_update_step[_dev] (state
+ * NULL: count / temperatures from the arguments) writing the next S rows
+ * pre-split into s16_next (Q = 4, 16-B aligned). */
+int trex_tree_split_x3(const float* X, int rows, int cols, int ldx, float max_abs, void* out,
+                       int ldo, void* stream);
+int trex_tree_gram_skip_x3p(const void* S16, int N, int64_t K, int skip_rows, float max_abs,
+                            float* G, void* workspace, int64_t workspace_bytes, void* stream);
+int trex_tree_mf_rows_x3p(const void* M16, int ldm, const void* S16, int N, int64_t K, int row0,
+                          int nrows, float max_abs_m, float max_abs_s, const void* codes,
+                          int64_t codes_bytes, int n_leaf, int Q, float* dS_rows, void* stream);
+int trex_adam_seq_update_step_x3p(const float* ds_anc, int n_anc, int L, int Q, float temperature,
+                                  float next_temperature, float* params, float* mu, float* nu,
+                                  int count, float lr, float b1, float b2, float eps,
+                                  const void* state, float max_abs_s, void* s16_next,
+                                  void* stream);
 
 /* compute_soft_cost (tree.py:212-266): ckind 0 = no C, 1 = C[Q] diagonal,
  * 2 = C[Q][Q]; W_scratch [N][L][Q] needed when ckind > 0. */

@@ -667,7 +667,8 @@ def test_fused_step_entries_are_bitwise_separate(device, dev_state):
         M = torch.empty_like(dA0)
         if fused:
             check(lib().trex_tree_surrogate_constraint(ptr(A), ptr(Gm), N, scale, T, s_ptr,
-                                                       ptr(loss), ptr(dA), ptr(M), ptr(ws), st))
+                                                       ptr(loss), ptr(dA), ptr(M), 0.0, None, 0,
+                                                       ptr(ws), st))
         else:
             check(lib().trex_tree_surrogate_combine(ptr(A), ptr(Gm), N, ptr(loss), ptr(dA), ptr(M),
                                                     ptr(ws), st))
@@ -723,3 +724,40 @@ def test_tree_device_loop_after_more_eager_steps(device):
     torch.cuda.synchronize()
     for k in ref.params:
         assert torch.equal(dut.params[k], ref.params[k]), k
+
+
+@pytest.mark.parametrize("nl,L,loop", [(100, 50, False), (256, 1001, False), (16, 52, True),
+                                       (40, 33, False)])
+def test_tree_optimizer_presplit_operands_are_bitwise_neutral(device, monkeypatch, nl, L, loop):
+    """x3 with pre-split GEMM operands (S16 / M16: trex_tree_split_x3,
+    trex_tree_gram_skip_x3p, trex_tree_mf_rows_x3p, the ancestors' pass
+    writing S16; the default) == TREX_PRESPLIT=0 (the GEMMs split f32
+    operands) bit for bit: losses, parameters and moments, eager or in the
+    captured device loop, with leaf codes (nl = 100: 96 code rows + 4 f32
+    rows), a ragged last column chunk (L = 1001) and no code rows (nl = 16)."""
+    params, noise, seqs = _tree_case(nl, L, 4, 41)
+    nz = _t(noise, device)
+    temps = [max(0.1, 2.0 * (1.0 - k / 20)) for k in range(12)]
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TREX_PRESPLIT", flag)
+        opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                              lr=0.02)
+        assert opt.presplit == (flag == "1")
+        if loop:
+            opt.step(temps[0], nz, temps[1])
+            lp = opt.device_loop(temps, 5, capture=True)
+            losses = [float(lp.run(1)) for _ in range(4)]
+            losses.append(float(opt.step(temps[5], nz, temps[7])))  # a temperature jump
+        else:
+            losses = [float(opt.step(temps[i], nz, temps[i + 1])) for i in range(3)]
+            losses.append(float(opt.step(temps[5], nz, temps[6])))
+        torch.cuda.synchronize()
+        runs.append((losses, {k: v.clone() for k, v in opt.params.items()},
+                     {k: v.clone() for k, v in opt.opt.mu.items()},
+                     {k: v.clone() for k, v in opt.opt.nu.items()}))
+    a, b = runs
+    assert a[0] == b[0]
+    for i in (1, 2, 3):
+        for k in a[i]:
+            assert torch.equal(a[i][k], b[i][k]), (i, k)

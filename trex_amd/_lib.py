@@ -93,7 +93,14 @@ SIGNATURES = {
     "trex_tree_leaf_codes": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _c_i64, _p, _p]),
     "trex_tree_mf_rows_x3_codes": (_c_i, [_p, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p,
                                           _c_i64, _c_i, _c_i, _p, _p]),
-    "trex_tree_surrogate_constraint": (_c_i, [_p, _p, _c_i, _c_f, _c_f, _p, _p, _p, _p, _p, _p]),
+    "trex_tree_surrogate_constraint": (_c_i, [_p, _p, _c_i, _c_f, _c_f, _p, _p, _p, _p, _c_f, _p,
+                                              _c_i, _p, _p]),
+    "trex_tree_split_x3": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _p, _c_i, _p]),
+    "trex_tree_gram_skip_x3p": (_c_i, [_p, _c_i, _c_i64, _c_i, _c_f, _p, _p, _c_i64, _p]),
+    "trex_tree_mf_rows_x3p": (_c_i, [_p, _c_i, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p,
+                                     _c_i64, _c_i, _c_i, _p, _p]),
+    "trex_adam_seq_update_step_x3p": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _c_f, _p, _p, _p, _c_i,
+                                             _c_f, _c_f, _c_f, _c_f, _p, _c_f, _p, _p]),
     "trex_tree_update_tree_bwd_adam": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_f, _p, _p, _p, _p, _c_i,
                                               _p, _c_f, _c_f, _c_f, _c_f, _p]),
     "trex_tree_soft_cost": (_c_i, [_p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _p, _c_i64, _p]),

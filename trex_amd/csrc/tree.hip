@@ -465,8 +465,31 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// f16x3 operand pre-split (x3p entry points, trex_tree_split_x3): every
+// group of 4 consecutive f32 values x * s is stored as 16 bytes -- the four
+// f16 hi parts, then the four f16 lo parts -- so a 16-B load of the
+// pre-split operand lands at the same byte offset as the f32 one and the
+// kernels stage it into LDS without the split arithmetic
+__device__ __forceinline__ u32x4 split_x3_group(float x0, float x1, float x2, float x3, float s) {
+  const float v[4] = {x0 * s, x1 * s, x2 * s, x3 * s};
+  h4 hi, lo;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hi[j] = (_Float16)v[j];
+    lo[j] = (_Float16)(v[j] - (float)hi[j]);
+  }
+  const uint2 a = __builtin_bit_cast(uint2, hi), b = __builtin_bit_cast(uint2, lo);
+  return (u32x4){a.x, a.y, b.x, b.y};
+}
+
+template <bool PRE = false>
 __device__ __forceinline__ void g3_stage(unsigned char* buf, int row, int sub, const u32x4& w,
                                          float sc) {
+  if constexpr (PRE) {
+    *reinterpret_cast<uint2*>(buf + row * kG3Stride + sub * 8) = uint2{w.x, w.y};
+    *reinterpret_cast<uint2*>(buf + row * kG3Stride + 32 + sub * 8) = uint2{w.z, w.w};
+    return;
+  }
   const float v[4] = {__uint_as_float(w.x) * sc, __uint_as_float(w.y) * sc,
                       __uint_as_float(w.z) * sc, __uint_as_float(w.w) * sc};
   h4 hi, lo;
@@ -479,6 +502,7 @@ __device__ __forceinline__ void g3_stage(unsigned char* buf, int row, int sub, c
   *reinterpret_cast<h4*>(buf + row * kG3Stride + 32 + sub * 8) = lo;
 }
 
+template <bool PRE = false>  // PRE: S pre-split (split_x3_group layout)
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gram_kernel3(
     const float* __restrict__ S, int N, int K, int ns, int t0s, int ntiles, int ngroups,
     int ksplit, int nchunks, float sc, float* __restrict__ part) {
@@ -521,7 +545,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const bool kv = 16 * c + 4 * sub < K;
 #pragma unroll
     for (int i = 0; i < kG3Rows / kRowsPerPass; ++i)
-      g3_stage(buf, rb + kRowsPerPass * i, sub, kv ? pf[i] : (u32x4){0u, 0u, 0u, 0u}, sc);
+      g3_stage<PRE>(buf, rb + kRowsPerPass * i, sub, kv ? pf[i] : (u32x4){0u, 0u, 0u, 0u}, sc);
   };
   const int lofs = r * kG3Stride + 16 * h;
   auto compute = [&](const unsigned char* buf) {
@@ -779,7 +803,9 @@ __global__ __launch_bounds__(256) void surrogate_combine_kernel(const float* __r
                                                                const float* __restrict__ G, int N,
                                                                float* __restrict__ dA,
                                                                float* __restrict__ M,
-                                                               double* __restrict__ rowloss) {
+                                                               double* __restrict__ rowloss,
+                                                               _Float16* __restrict__ M16 = nullptr,
+                                                               int ldm = 0, float sm = 1.0f) {
   __shared__ double sh[256];
   const int i = blockIdx.x;
   const float gii = G[(size_t)i * N + i];
@@ -800,8 +826,22 @@ __global__ __launch_bounds__(256) void surrogate_combine_kernel(const float* __r
   if (M) {
     for (int j = threadIdx.x; j < N; j += 256) {
       const float a = A[(size_t)i * N + j] + A[(size_t)j * N + i];
-      M[(size_t)i * N + j] = (i == j ? (float)rc : 0.0f) - a;
+      const float m = (i == j ? (float)rc : 0.0f) - a;
+      M[(size_t)i * N + j] = m;
+      if (M16) {  // the pre-split copy (split_x3_group layout, zero past N)
+        const float v = m * sm;
+        const _Float16 hi = (_Float16)v;
+        _Float16* g = M16 + ((size_t)i * (ldm / 4) + (j >> 2)) * 8 + (j & 3);
+        g[0] = hi;
+        g[4] = (_Float16)(v - (float)hi);
+      }
     }
+    if (M16)
+      for (int j = N + threadIdx.x; j < ldm; j += 256) {
+        _Float16* g = M16 + ((size_t)i * (ldm / 4) + (j >> 2)) * 8 + (j & 3);
+        g[0] = (_Float16)0.0f;
+        g[4] = (_Float16)0.0f;
+      }
   }
 }
 
@@ -1149,11 +1189,13 @@ __device__ __forceinline__ h8 tr_pair(const unsigned char* p, int four_rows) {
 // an F item = one site's 4 states = one byte) instead of F and expand them
 // into the same f16 hi / lo planes (one-hot x sf is exact in f16, lo = 0):
 // bitwise the same result, a quarter of the bytes for those stages
-template <int TPC, bool CODES>
+// PRE: M and F pre-split (split_x3_group layout; M rows ldm elements apart,
+// zero past N): the stages copy them into LDS without the split arithmetic
+template <int TPC, bool CODES, bool PRE = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void mf_kernel3(
     const float* __restrict__ Mm, const float* __restrict__ F, int N, int K, int row0, int nrows,
     int nchunks, float* __restrict__ out, float sm, float sf, const uint8_t* __restrict__ codesR,
-    int lcs) {
+    int lcs, int ldm) {
   constexpr int CW = TPC * 32;
   constexpr int NIT = 32 * (CW / 4);  // F (row, column group) float4 items per stage
   constexpr int IPT = (NIT + 511) / 512;
@@ -1168,7 +1210,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
   const int rbase = blockIdx.y * 256 + wave * 32;
-  const rsrc_t rm = make_rsrc(Mm, (uint32_t)((size_t)N * N * 4));
+  const rsrc_t rm = make_rsrc(Mm, (uint32_t)((size_t)N * ldm * 4));
   const rsrc_t rf = make_rsrc(F, (uint32_t)((size_t)N * K * 4));
   // CODES: item (n, cg) reads the code byte of row n, site chunk * CW / 4 + cg
   // (sites past L read the next row's bytes: columns past K, never stored)
@@ -1196,7 +1238,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int rg = blockIdx.y * 256 + mrow + 64 * i;
-    mvb[i] = rg < nrows ? ((row0 + rg) * N + 4 * mseg) * 4 : -1;
+    mvb[i] = rg < nrows ? ((row0 + rg) * ldm + 4 * mseg) * 4 : -1;
   }
   const int nst = (N + 31) / 32;
   const int cnt = blockIdx.x < nchunks ? (nchunks - 1 - (int)blockIdx.x) / gx + 1 : 0;
@@ -1247,6 +1289,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int j = 0; j < IPT; ++j) {
       if (!fok[j] || (CODES && q.s < lcs)) continue;
+      if constexpr (PRE) {
+        *reinterpret_cast<uint2*>(buf + lofs[j]) = uint2{q.a[j].x, q.a[j].y};
+        *reinterpret_cast<uint2*>(buf + FPLANE + lofs[j]) = uint2{q.a[j].z, q.a[j].w};
+        continue;
+      }
       const uint32_t e[4] = {q.a[j].x, q.a[j].y, q.a[j].z, q.a[j].w};
       h4 hi, lo;
 #pragma unroll
@@ -1261,6 +1308,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     unsigned char* mb = buf + FBUF;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+      if constexpr (PRE) {
+        unsigned char* rowp = mb + (mrow + 64 * i) * kMfStride + 8 * mseg;
+        *reinterpret_cast<uint2*>(rowp) = uint2{q.m[i].x, q.m[i].y};
+        *reinterpret_cast<uint2*>(rowp + 64) = uint2{q.m[i].z, q.m[i].w};
+        continue;
+      }
       const uint32_t e[4] = {q.m[i].x, q.m[i].y, q.m[i].z, q.m[i].w};
       h4 hi, lo;
 #pragma unroll
@@ -2008,6 +2061,52 @@ __global__ __launch_bounds__(256) void adam_seq_update4_kernel(
 
 int grid_for(int64_t n, int per = 256, int cap = 8192);
 
+// x3p operands: rows x cols of X (row stride ldx) -> split_x3_group layout,
+// ldo f32-equivalent columns per row (groups past cols are zero)
+__global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__ X, int rows,
+                                                      int cols, int ldx, float s,
+                                                      u32x4* __restrict__ out, int ldo) {
+  const int G = ldo / 4;
+  const int64_t n = (int64_t)rows * G;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
+    const int row = (int)(t / G), c = 4 * (int)(t % G);
+    const float* x = X + (size_t)row * ldx;
+    out[t] = split_x3_group(c < cols ? x[c] : 0.0f, c + 1 < cols ? x[c + 1] : 0.0f,
+                            c + 2 < cols ? x[c + 2] : 0.0f, c + 3 < cols ? x[c + 3] : 0.0f, s);
+  }
+}
+
+// the Q = 4 ancestors' pass writing the next S rows pre-split (x3p)
+__global__ __launch_bounds__(256) void adam_seq_update4_x3p_kernel(
+    const fv4* __restrict__ ds, int64_t rows, float T, float Tn, fv4* __restrict__ p,
+    fv4* __restrict__ mu, fv4* __restrict__ nu, float lr, float b1, float b2, float eps,
+    float bc1, float bc2, float sx, fv4* __restrict__ s_out, const StepState* __restrict__ ss) {
+  if (ss) {
+    bc1 = ss->bc1;
+    bc2 = ss->bc2;
+    T = ss->T;
+    Tn = ss->Tn;
+  }
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  const fv4 d = __builtin_nontemporal_load(ds + r), a = __builtin_nontemporal_load(p + r);
+  const fv4 m = __builtin_nontemporal_load(mu + r), v = __builtin_nontemporal_load(nu + r);
+  float p4[4], g4[4], m4[4], v4[4], s4[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    p4[q] = a[q];
+    g4[q] = d[q];
+    m4[q] = m[q];
+    v4[q] = v[q];
+  }
+  adam_seq_row4(g4, p4, m4, v4, T, Tn, lr, b1, b2, eps, bc1, bc2, s4);
+  __builtin_nontemporal_store((fv4){p4[0], p4[1], p4[2], p4[3]}, p + r);
+  __builtin_nontemporal_store((fv4){m4[0], m4[1], m4[2], m4[3]}, mu + r);
+  __builtin_nontemporal_store((fv4){v4[0], v4[1], v4[2], v4[3]}, nu + r);
+  __builtin_nontemporal_store(__builtin_bit_cast(fv4, split_x3_group(s4[0], s4[1], s4[2], s4[3], sx)),
+                              s_out + r);
+}
+
 void launch_adam_seq(const float* ds, int64_t rows, int Q, float T, float Tn, float* p, float* mu,
                      float* nu, float lr, float b1, float b2, float eps, float bc1, float bc2,
                      float* s_out, const StepState* ss, hipStream_t st) {
@@ -2222,26 +2321,30 @@ float split_scale(float max_abs) {
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
-         hipStream_t st, int t0 = 0, float x3_max = 0.0f) {
+         hipStream_t st, int t0 = 0, float x3_max = 0.0f, bool pre = false) {
   const GramPlan g = gram_plan(N, K, symmetric != 0, t0);
   if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
   const int blocks = g.npairs * ks8;
   // v5 serves both precisions; v3 (TREX_GRAM=3) only the x3 one
   const bool x3 = x3_max > 0.0f;
-  const int gv = gram_version(x3);
+  const int gv = pre ? 3 : gram_version(x3);  // pre-split operands: the v3 kernel
+  if (pre && !(x3 && symmetric && X == Y && gram3_ok(N, K)))
+    return set_error(TREX_E_UNSUPPORTED, "gram: no pre-split kernel for this shape");
   if (symmetric && X == Y && gram3_ok(N, K) && (x3 || gv >= 5)) {
     int T5 = 0;
     const bool v5 = gv >= 5;
     const int W = (gv == 6 && x3) ? 8 : kG5Waves;
     const Gram3Plan p = v5 ? gram5_plan(N, K, 2 * t0, &T5, W) : gram3_plan(N, K, 2 * t0);
     if (p.ntiles == 0) return TREX_OK;
-    static bool lds_set = false;
-    if (!lds_set) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3),
+    static const bool lds_set = [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
-      lds_set = true;
-    }
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
+      return true;
+    }();
+    (void)lds_set;
     const float sc = x3 ? split_scale(x3_max) : 1.0f;
     if (v5) {
       const dim3 grid(((p.ksplit + 7) / 8 * 8) * p.ngroups);
@@ -2296,9 +2399,13 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
         else go(gram_kernel5<16, false>);
       }
     } else {
-      hipLaunchKernelGGL(gram_kernel3, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds,
-                         st, X, N, (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks,
-                         sc, part);
+      auto go3 = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds, st, X,
+                           N, (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks, sc,
+                           part);
+      };
+      if (pre) go3(gram_kernel3<true>);
+      else go3(gram_kernel3<false>);
     }
     hipLaunchKernelGGL(gram3_reduce_kernel, dim3(p.ntiles * 16), dim3(256), 0, st, part, N, p.ns,
                        p.t0s, p.ntiles, p.ksplit, G);
@@ -2572,6 +2679,32 @@ extern "C" int trex_adam_seq_update_step_dev(const float* ds_anc, int n_anc, int
   return tree_hip_check("trex_adam_seq_update_step_dev");
 }
 
+extern "C" int trex_adam_seq_update_step_x3p(const float* ds_anc, int n_anc, int L, int Q,
+                                             float temperature, float next_temperature,
+                                             float* params, float* mu, float* nu, int count,
+                                             float lr, float b1, float b2, float eps,
+                                             const void* state, float max_abs_s, void* s16_next,
+                                             void* stream) {
+  if (!ds_anc || !params || !mu || !nu || !s16_next || n_anc <= 0 || L <= 0 || Q != 4 ||
+      !pos_finite_f32(max_abs_s) ||
+      (!state && (count < 1 || !pos_finite_f32(temperature) ||
+                  !pos_finite_f32(next_temperature))) ||
+      ((reinterpret_cast<uintptr_t>(ds_anc) | reinterpret_cast<uintptr_t>(params) |
+        reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
+        reinterpret_cast<uintptr_t>(s16_next)) & 15) != 0)
+    return set_error(TREX_E_ARG, "trex_adam_seq_update_step_x3p: bad arguments");
+  const int64_t rows = (int64_t)n_anc * L;
+  const float bc1 = state ? 1.0f : bias_corr(b1, count);
+  const float bc2 = state ? 1.0f : bias_corr(b2, count);
+  hipLaunchKernelGGL(adam_seq_update4_x3p_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256),
+                     0, (hipStream_t)stream, reinterpret_cast<const fv4*>(ds_anc), rows,
+                     temperature, next_temperature, reinterpret_cast<fv4*>(params),
+                     reinterpret_cast<fv4*>(mu), reinterpret_cast<fv4*>(nu), lr, b1, b2, eps, bc1,
+                     bc2, split_scale(max_abs_s), static_cast<fv4*>(s16_next),
+                     static_cast<const StepState*>(state));
+  return tree_hip_check("trex_adam_seq_update_step_x3p");
+}
+
 extern "C" int trex_sq_norm_parts(const float* x, int64_t n, double* parts, int n_parts,
                                   void* stream) {
   if (!x || !parts || n_parts <= 0 || n_parts > 8192)
@@ -2634,9 +2767,10 @@ extern "C" int trex_tree_gram(const float* S, int N, int64_t K, float* G, void* 
 
 extern "C" int trex_tree_surrogate_constraint(const float* A, const float* G, int N, float scale,
                                               float grad_scale, const void* state, float* loss,
-                                              float* dA, float* M, void* workspace,
-                                              void* stream) {
-  if (!A || !G || !loss || !dA || !M || !workspace || N < 3)
+                                              float* dA, float* M, float max_abs_m, void* M16,
+                                              int ldm16, void* workspace, void* stream) {
+  if (!A || !G || !loss || !dA || !M || !workspace || N < 3 ||
+      (M16 && (ldm16 < N || ldm16 % 4 != 0 || !pos_finite_f32(max_abs_m))))
     return set_error(TREX_E_ARG, "trex_tree_surrogate_constraint: bad arguments");
   const int n_anc = (N - 1) / 2;
   hipStream_t st = (hipStream_t)stream;
@@ -2644,7 +2778,8 @@ extern "C" int trex_tree_surrogate_constraint(const float* A, const float* G, in
   double* colloss = rowloss + N;
   const StepState* ss = static_cast<const StepState*>(state);
   hipLaunchKernelGGL(surrogate_combine_kernel, dim3(N), dim3(256), 0, st, A, G, N, dA, M,
-                     rowloss);
+                     rowloss, static_cast<_Float16*>(M16), ldm16,
+                     M16 ? split_scale(max_abs_m) : 1.0f);
   hipLaunchKernelGGL(constraint_kernel, dim3(n_anc), dim3(256), 0, st, A, N, scale, grad_scale,
                      colloss, dA, ss);
   hipLaunchKernelGGL(sum_rows2_kernel, dim3(1), dim3(256), 0, st, rowloss, N, colloss, n_anc,
@@ -2668,7 +2803,7 @@ extern "C" int trex_tree_surrogate_combine(const float* A, const float* G, int N
 namespace {
 int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int row0, int nrows,
           float max_abs_m, float max_abs_s, float* dS_rows, const uint8_t* codesR, int lcs,
-          void* stream, bool x3);
+          void* stream, bool x3, bool pre = false, int ldm = 0);
 }  // namespace
 extern "C" int trex_tree_mf_rows(const float* M, const float* S, int N, int64_t K, int row0,
                                  int nrows, float* dS_rows, void* stream) {
@@ -2695,7 +2830,8 @@ namespace {
 // v3 MF launch; codesR / lcs: leaf-code stages (CODES instantiation) or null / 0
 int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int row0, int nrows,
           float max_abs_m, float max_abs_s, float* dS_rows, const uint8_t* codesR, int lcs,
-          void* stream, bool x3) {
+          void* stream, bool x3, bool pre, int ldm) {
+  if (!pre) ldm = N;
   if (!M || !S || !dS_rows || N <= 0 || K <= 0 || K > 0x7FFFFFFF || row0 < 0 || nrows <= 0 ||
       row0 + nrows > N || !pos_finite_f32(max_abs_m) || !pos_finite_f32(max_abs_s))
     return set_error(TREX_E_ARG, "%s: bad arguments", fn);
@@ -2725,7 +2861,7 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
     const int gx = std::max(1, std::min(nch, std::max(1, cu_count() / rg)));
     hipLaunchKernelGGL(kernel, dim3(gx, rg), dim3(512), lds, (hipStream_t)stream, M, S, N,
                        (int)K, row0, nrows, nch, dS_rows, split_scale(max_abs_m),
-                       split_scale(max_abs_s), codesR, lcs);
+                       split_scale(max_abs_s), codesR, lcs, ldm);
   };
   const int lds = 2 * (2 * 32 * 320 + 256 * kMfStride);
   const bool codes = codesR && lcs > 0;
@@ -2735,6 +2871,18 @@ int mf_x3(const char* fn, const float* M, const float* S, int N, int64_t K, int 
   const bool v5_ok = 32LL * K * 4 < 0x7FFFFFF0LL;
   if (!x3 && !v5_ok) return set_error(TREX_E_UNSUPPORTED, "%s: K too large for the f32 v5 MF", fn);
   // f32: v5; x3: v3 (v5 measured 242 vs 224 us with leaf codes at C5) unless TREX_MF=5
+  if (pre) {  // pre-split operands: the v3 kernel
+    if (!x3 || ldm < N || ldm % 32 != 0 || (int64_t)N * ldm * 4 > 0x7FFFFFF0LL)
+      return set_error(TREX_E_ARG, "%s: bad pre-split M stride", fn);
+    if (best == 5) {
+      if (codes) go(mf_kernel3<5, true, true>, 5, lds);
+      else go(mf_kernel3<5, false, true>, 5, lds);
+    } else {
+      if (codes) go(mf_kernel3<4, true, true>, 4, lds);
+      else go(mf_kernel3<4, false, true>, 4, lds);
+    }
+    return tree_hip_check(fn);
+  }
   if (v5_ok && (!x3 || (ev && std::atoi(ev) == 5))) {
     // f32: the transposed F slice is CW x 144 B
     const int lds5 = x3 ? lds : 2 * (160 * kMfStride + 256 * kMfStride);
@@ -2840,6 +2988,49 @@ extern "C" int trex_tree_mf_rows_x3_codes(const float* M, const float* S, int N,
                                  "trex_tree_leaf_codes_bytes(n_leaf, K / Q)");
   return mf_x3("trex_tree_mf_rows_x3_codes", M, S, N, K, row0, nrows, max_abs_m, max_abs_s,
                dS_rows, static_cast<const uint8_t*>(codes), lcr / 32, stream, true);
+}
+
+extern "C" int trex_tree_split_x3(const float* X, int rows, int cols, int ldx, float max_abs,
+                                  void* out, int ldo, void* stream) {
+  if (!X || !out || rows <= 0 || cols <= 0 || ldx < cols || ldo < cols || ldo % 4 != 0 ||
+      !pos_finite_f32(max_abs) || (reinterpret_cast<uintptr_t>(out) & 15) != 0)
+    return set_error(TREX_E_ARG, "trex_tree_split_x3: bad arguments");
+  const int64_t n = (int64_t)rows * (ldo / 4);
+  hipLaunchKernelGGL(split_x3_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 65536)),
+                     dim3(256), 0, (hipStream_t)stream, X, rows, cols, ldx, split_scale(max_abs),
+                     static_cast<u32x4*>(out), ldo);
+  return tree_hip_check("trex_tree_split_x3");
+}
+
+extern "C" int trex_tree_gram_skip_x3p(const void* S16, int N, int64_t K, int skip_rows,
+                                       float max_abs, float* G, void* workspace,
+                                       int64_t workspace_bytes, void* stream) {
+  if (!S16 || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF || skip_rows < 0 ||
+      skip_rows > N || !pos_finite_f32(max_abs) || K % 4 != 0)
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3p: bad arguments");
+  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3p: workspace too small");
+  const float* S = static_cast<const float*>(S16);
+  return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream,
+              skip_rows / 64, max_abs, true);
+}
+
+extern "C" int trex_tree_mf_rows_x3p(const void* M16, int ldm, const void* S16, int N, int64_t K,
+                                     int row0, int nrows, float max_abs_m, float max_abs_s,
+                                     const void* codes, int64_t codes_bytes, int n_leaf, int Q,
+                                     float* dS_rows, void* stream) {
+  const char* fn = "trex_tree_mf_rows_x3p";
+  if (K % 4 != 0 || (codes && Q != 4)) return set_error(TREX_E_ARG, "%s: bad arguments", fn);
+  int lcs = 0;
+  if (codes) {
+    const int lcr = trex_tree_leaf_code_rows(n_leaf);
+    if (lcr <= 0 || lcr > N || codes_bytes < (int64_t)lcr * (K / Q))
+      return set_error(TREX_E_ARG, "%s: bad codes", fn);
+    lcs = lcr / 32;
+  }
+  return mf_x3(fn, static_cast<const float*>(M16), static_cast<const float*>(S16), N, K, row0,
+               nrows, max_abs_m, max_abs_s, dS_rows, static_cast<const uint8_t*>(codes), lcs,
+               stream, true, true, ldm);
 }
 
 extern "C" int trex_tree_mf(const float* M, const float* S, int N, int64_t K, float* dS,

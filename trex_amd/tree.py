@@ -456,6 +456,68 @@ class TreeOptimizer:
                                              cb.numel(), ptr(status), stream_handle(dev)))
             if int(status.item()) == 0:
                 self.codes = cb
+        # x3 without clipping: the GEMM operands are kept pre-split (S16, M16:
+        # trex_tree_split_x3's layout) -- the ancestors' pass writes the next
+        # S rows split, the surrogate writes M split, and the GEMMs stage
+        # them without the split arithmetic (bitwise the x3 path;
+        # TREX_PRESPLIT=0 keeps the f32 operands)
+        self.presplit = (self.gemm == "x3" and clip_norm is None and self.Q == 4
+                         and os.environ.get("TREX_PRESPLIT", "1") != "0")
+        if self.presplit:
+            self.S16 = torch.empty_like(self.S)
+            self.ldm = (self.N + 31) // 32 * 32
+            self.M16 = torch.zeros((self.N, self.ldm), **f32)
+            check(lib().trex_tree_split_x3(ptr(self.S), self.N, self.K, self.K, 1.0,
+                                           ptr(self.S16), self.K, stream_handle(dev)))
+
+    def _split_anc(self, st):
+        """S16's ancestor rows from S's (after update_seq rewrote them)."""
+        check(lib().trex_tree_split_x3(ptr(self.S[self.n_leaf:]), self.n_anc, self.K, self.K, 1.0,
+                                       ptr(self.S16[self.n_leaf:]), self.K, st))
+
+    def _gram(self, st):
+        N, K = self.N, self.K
+        if self.presplit:
+            check(lib().trex_tree_gram_skip_x3p(ptr(self.S16), N, K, self.skip_rows, 1.0,
+                                                ptr(self.G), ptr(self.ws), self.ws.numel(), st))
+        elif self.gemm == "x3":
+            check(lib().trex_tree_gram_skip_x3(ptr(self.S), N, K, self.skip_rows, 1.0,
+                                               ptr(self.G), ptr(self.ws), self.ws.numel(), st))
+        else:
+            check(lib().trex_tree_gram_skip(ptr(self.S), N, K, self.skip_rows, ptr(self.G),
+                                            ptr(self.ws), self.ws.numel(), st))
+
+    def _combine(self, st, grad_scale, state):
+        """surrogate loss / dA / M (and M16), graph constraint, one reduce."""
+        check(lib().trex_tree_surrogate_constraint(
+            ptr(self.A), ptr(self.G), self.N, self.scale, grad_scale, state, ptr(self.loss),
+            ptr(self.dA), ptr(self.M), float(self.N + 1),
+            ptr(self.M16) if self.presplit else None, self.ldm if self.presplit else 0,
+            ptr(self.ws), st))
+
+    def _mf(self, st):
+        """d loss / dS for the ancestor rows only (leaf rows are fixed data)."""
+        L_ = lib()
+        N, K = self.N, self.K
+        dS = self.dS[self.n_leaf:]
+        if self.presplit:
+            cb = self.codes
+            check(L_.trex_tree_mf_rows_x3p(ptr(self.M16), self.ldm, ptr(self.S16), N, K,
+                                           self.n_leaf, self.n_anc, float(N + 1), 1.0,
+                                           ptr(cb) if cb is not None else None,
+                                           cb.numel() if cb is not None else 0, self.n_leaf,
+                                           self.Q, ptr(dS), st))
+        elif self.codes is not None:
+            check(L_.trex_tree_mf_rows_x3_codes(ptr(self.M), ptr(self.S), N, K, self.n_leaf,
+                                                self.n_anc, float(N + 1), 1.0, ptr(self.codes),
+                                                self.codes.numel(), self.n_leaf, self.Q, ptr(dS),
+                                                st))
+        elif self.gemm == "x3":
+            check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
+                                          float(N + 1), 1.0, ptr(dS), st))
+        else:
+            check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
+                                       ptr(dS), st))
 
     def step(self, temperature: float, noise, next_temperature=None):
         """One optimisation step; returns the (device) loss before the update.
@@ -470,39 +532,23 @@ class TreeOptimizer:
         st = stream_handle(self.S.device)
         T = float(temperature)
         p = self.params
-        N, K = self.N, self.K
+        N = self.N
         if self._s_temperature != T:
             check(L_.trex_tree_update_seq(ptr(p["ancestors"]), self.n_anc, self.L, self.Q, T,
                                           ptr(self.S[self.n_leaf:]), st))
+            if self.presplit:
+                self._split_anc(st)
         self._s_temperature = None
         check(L_.trex_tree_update_tree(ptr(p["tree_params"]), ptr(noise), None, N, self.n_anc,
                                        1.0, ptr(self.A), st))
-        if self.gemm == "x3":
-            check(L_.trex_tree_gram_skip_x3(ptr(self.S), N, K, self.skip_rows, 1.0, ptr(self.G),
-                                            ptr(self.ws), self.ws.numel(), st))
-        else:
-            check(L_.trex_tree_gram_skip(ptr(self.S), N, K, self.skip_rows, ptr(self.G),
-                                         ptr(self.ws), self.ws.numel(), st))
+        self._gram(st)
         if self.reducer is not None:
             self.reducer(self.G[self.g_row0:])
             check(L_.trex_tree_gram_mirror(ptr(self.G), N, self.g_row0, st))
         # surrogate loss / dA / M, then the graph constraint (loss and dA
         # accumulated), one reduce for both
-        check(L_.trex_tree_surrogate_constraint(ptr(self.A), ptr(self.G), N, self.scale, T, None,
-                                                ptr(self.loss), ptr(self.dA), ptr(self.M),
-                                                ptr(self.ws), st))
-        # d loss / dS for the ancestor rows only (leaf rows are fixed data)
-        if self.codes is not None:
-            check(L_.trex_tree_mf_rows_x3_codes(ptr(self.M), ptr(self.S), N, K, self.n_leaf,
-                                                self.n_anc, float(N + 1), 1.0, ptr(self.codes),
-                                                self.codes.numel(), self.n_leaf, self.Q,
-                                                ptr(self.dS[self.n_leaf:]), st))
-        elif self.gemm == "x3":
-            check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
-                                          float(N + 1), 1.0, ptr(self.dS[self.n_leaf:]), st))
-        else:
-            check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, self.n_leaf, self.n_anc,
-                                       ptr(self.dS[self.n_leaf:]), st))
+        self._combine(st, T, None)
+        self._mf(st)
         if self.opt.clip is None:
             o = self.opt
             o.count += 1
@@ -520,11 +566,18 @@ class TreeOptimizer:
             # ... and update_seq of the next step folded in (S rows rewritten
             # in place from the new logits)
             Tn = T if next_temperature is None else float(next_temperature)
-            check(L_.trex_adam_seq_update_step(ptr(self.dS[self.n_leaf:]), self.n_anc, self.L,
-                                               self.Q, T, Tn, ptr(p["ancestors"]),
-                                               ptr(o.mu["ancestors"]), ptr(o.nu["ancestors"]),
-                                               o.count, float(o.lr), float(o.b1), float(o.b2),
-                                               float(o.eps), ptr(self.S[self.n_leaf:]), st))
+            if self.presplit:
+                check(L_.trex_adam_seq_update_step_x3p(
+                    ptr(self.dS[self.n_leaf:]), self.n_anc, self.L, self.Q, T, Tn,
+                    ptr(p["ancestors"]), ptr(o.mu["ancestors"]), ptr(o.nu["ancestors"]), o.count,
+                    float(o.lr), float(o.b1), float(o.b2), float(o.eps), None, 1.0,
+                    ptr(self.S16[self.n_leaf:]), st))
+            else:
+                check(L_.trex_adam_seq_update_step(
+                    ptr(self.dS[self.n_leaf:]), self.n_anc, self.L, self.Q, T, Tn,
+                    ptr(p["ancestors"]), ptr(o.mu["ancestors"]), ptr(o.nu["ancestors"]), o.count,
+                    float(o.lr), float(o.b1), float(o.b2), float(o.eps),
+                    ptr(self.S[self.n_leaf:]), st))
             self._s_temperature = Tn
         else:
             check(L_.trex_tree_update_tree_bwd(ptr(self.A), ptr(self.dA), None, N, self.n_anc,
@@ -621,6 +674,8 @@ class _TreeDeviceLoop:
             check(lib().trex_tree_update_seq(ptr(opt.params["ancestors"]), opt.n_anc, opt.L,
                                              opt.Q, T0, ptr(opt.S[opt.n_leaf:]),
                                              stream_handle(dev)))
+            if opt.presplit:
+                opt._split_anc(stream_handle(dev))
             opt._s_temperature = T0
         if capture:
             # capture records launches without running them: the state
@@ -634,7 +689,7 @@ class _TreeDeviceLoop:
         L_ = lib()
         st = stream_handle(o.S.device)
         p = o.params
-        N, K = o.N, o.K
+        N = o.N
         a = o.opt
         state = ptr(a.state)
         check(L_.trex_step_advance(state, float(a.b1), float(a.b2), ptr(self.temps), self.n_temps,
@@ -642,32 +697,25 @@ class _TreeDeviceLoop:
         check(L_.trex_gumbel_noise(self.seed, state, self.noise.numel(), ptr(self.noise), st))
         check(L_.trex_tree_update_tree(ptr(p["tree_params"]), ptr(self.noise), None, N, o.n_anc,
                                        1.0, ptr(o.A), st))
-        if o.gemm == "x3":
-            check(L_.trex_tree_gram_skip_x3(ptr(o.S), N, K, o.skip_rows, 1.0, ptr(o.G),
-                                            ptr(o.ws), o.ws.numel(), st))
-        else:
-            check(L_.trex_tree_gram_skip(ptr(o.S), N, K, o.skip_rows, ptr(o.G), ptr(o.ws),
-                                         o.ws.numel(), st))
-        check(L_.trex_tree_surrogate_constraint(ptr(o.A), ptr(o.G), N, o.scale, 0.0, state,
-                                                ptr(o.loss), ptr(o.dA), ptr(o.M), ptr(o.ws), st))
+        o._gram(st)
+        o._combine(st, 0.0, state)
         dS = o.dS[o.n_leaf:]
-        if o.codes is not None:
-            check(L_.trex_tree_mf_rows_x3_codes(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc,
-                                                float(N + 1), 1.0, ptr(o.codes), o.codes.numel(),
-                                                o.n_leaf, o.Q, ptr(dS), st))
-        elif o.gemm == "x3":
-            check(L_.trex_tree_mf_rows_x3(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc,
-                                          float(N + 1), 1.0, ptr(dS), st))
-        else:
-            check(L_.trex_tree_mf_rows(ptr(o.M), ptr(o.S), N, K, o.n_leaf, o.n_anc, ptr(dS), st))
+        o._mf(st)
         check(L_.trex_tree_update_tree_bwd_adam(
             ptr(o.A), ptr(o.dA), None, N, o.n_anc, 1.0, ptr(o.grads["tree_params"]),
             ptr(p["tree_params"]), ptr(a.mu["tree_params"]), ptr(a.nu["tree_params"]), 0, state,
             float(a.lr), float(a.b1), float(a.b2), float(a.eps), st))
-        check(L_.trex_adam_seq_update_step_dev(ptr(dS), o.n_anc, o.L, o.Q, state,
-                                               ptr(p["ancestors"]), ptr(a.mu["ancestors"]),
-                                               ptr(a.nu["ancestors"]), float(a.lr), float(a.b1),
-                                               float(a.b2), float(a.eps), ptr(o.S[o.n_leaf:]), st))
+        if o.presplit:
+            check(L_.trex_adam_seq_update_step_x3p(
+                ptr(dS), o.n_anc, o.L, o.Q, 1.0, 1.0, ptr(p["ancestors"]),
+                ptr(a.mu["ancestors"]), ptr(a.nu["ancestors"]), 0, float(a.lr), float(a.b1),
+                float(a.b2), float(a.eps), state, 1.0, ptr(o.S16[o.n_leaf:]), st))
+        else:
+            check(L_.trex_adam_seq_update_step_dev(ptr(dS), o.n_anc, o.L, o.Q, state,
+                                                   ptr(p["ancestors"]), ptr(a.mu["ancestors"]),
+                                                   ptr(a.nu["ancestors"]), float(a.lr),
+                                                   float(a.b1), float(a.b2), float(a.eps),
+                                                   ptr(o.S[o.n_leaf:]), st))
 
     def run(self, n_steps: int):
         """n_steps steps (graph replays or eager launches); returns the
