@@ -73,3 +73,31 @@ def test_leaf_code_mf_rejects_wrong_alphabet_or_short_buffer(Q, short):
                                       need - 1 if short else need, n_leaf, Q, p, None)
     assert rc == TREX_E_ARG, rc
     assert b"codes" in L.trex_last_error()
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf"), 0.0, -2.0])
+def test_presplit_and_fused_step_entries_reject_bad_args(bad):
+    """The x3p (pre-split operand) entry points and the fused C5 step entry
+    points reject bad bounds / temperatures / shapes before any launch."""
+    b = _buf()
+    p = b.ctypes.data
+    L = lib()
+    ws = int(L.trex_tree_workspace_bytes(64, 256))
+    w = _buf(ws)
+    assert L.trex_tree_split_x3(p, 64, 256, 256, bad, p, 256, None) == TREX_E_ARG
+    assert L.trex_tree_split_x3(p, 64, 256, 256, 1.0, p, 254, None) == TREX_E_ARG  # ldo % 4
+    assert L.trex_tree_gram_skip_x3p(p, 64, 256, 0, bad, p, w.ctypes.data, ws, None) == TREX_E_ARG
+    assert L.trex_tree_mf_rows_x3p(p, 64, p, 64, 256, 0, 64, bad, 1.0, None, 0, 32, 4, p,
+                                   None) == TREX_E_ARG
+    assert L.trex_tree_mf_rows_x3p(p, 64, p, 64, 258, 0, 64, 65.0, 1.0, None, 0, 32, 4, p,
+                                   None) == TREX_E_ARG  # K % 4
+    assert L.trex_adam_seq_update_step_x3p(p, 8, 16, 4, bad, 1.0, p, p, p, 1, 0.01, 0.9, 0.999,
+                                           1e-8, None, 1.0, p, None) == TREX_E_ARG
+    assert L.trex_adam_seq_update_step_x3p(p, 8, 16, 5, 1.0, 1.0, p, p, p, 1, 0.01, 0.9, 0.999,
+                                           1e-8, None, 1.0, p, None) == TREX_E_ARG  # Q = 4 only
+    assert L.trex_tree_update_tree_bwd_adam(p, p, None, 7, 3, bad, p, p, p, p, 1, None, 0.01,
+                                            0.9, 0.999, 1e-8, None) == TREX_E_ARG
+    assert L.trex_tree_update_tree_bwd_adam(p, p, None, 7, 3, 1.0, p, p, p, p, 0, None, 0.01,
+                                            0.9, 0.999, 1e-8, None) == TREX_E_ARG  # count 0
+    assert L.trex_tree_surrogate_constraint(p, p, 7, 10.0, 1.0, None, p, p, p, 8.0, p, 6,
+                                            w.ctypes.data, None) == TREX_E_ARG  # ldm16 < N
