@@ -40,6 +40,14 @@ extern "C" {
 
 /* flags for trex_sankoff_fwd / trex_sankoff_bwd */
 #define TREX_FLAG_HARD_ROOT 1u  /* tau>0: site score = min(D_root), not smin */
+/* 4 < Q <= 20 softmin: the lane-per-site kernel decides on the device, from
+ * the cost matrix, whether it takes a call (a gate in the state-parallel
+ * launch writes K, K^T and a flag into the workspace).  A caller that reused
+ * the workspace with the same cost and tau and read that flag as set
+ * (int32 at byte trex_site_flag_offset(B, L, Q) of the workspace) may pass
+ * TREX_FLAG_SITE_REUSE: the gate launch is skipped.  Any other call on the
+ * workspace may overwrite K and the flag. */
+#define TREX_FLAG_SITE_REUSE 2u
 
 /* plan layout constants (see trex_plan_build).  A plan holds, after the
  * header, the forward steps [B][n_int][4], the backtrack entries
@@ -66,6 +74,7 @@ const char* trex_last_error(void);
  *    v4 plans must re-query it), Q up to 64, ragged Q > 4.
  * 4: site-major DP tables. */
 int trex_version(void);
+int64_t trex_site_flag_offset(int B, int L, int Q); /* -1 when Q has no site kernel */
 
 /* ------------------------------------------------------------------------
  * Topology plan (host side; topology is static per call like trex's jit

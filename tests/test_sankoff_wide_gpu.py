@@ -267,3 +267,34 @@ def test_c3_scale_properties(device):
     assert float(h.tree_score[0]) == float(r[2])
     np.testing.assert_array_equal(h.dp.cpu().numpy()[0], r[1][:, n:, :].transpose(1, 0, 2))
     np.testing.assert_array_equal(anc.astype(np.float32), r[0][n:])
+
+
+@pytest.mark.parametrize("tau", [0.5, 0.02])  # 0.02: range / tau > 40, the gate refuses
+def test_site_gate_reuse_is_bitwise_neutral(device, tau, wide_kernel):
+    """SankoffEngine passes TREX_FLAG_SITE_REUSE (no gate launch) once a
+    (cost tensor, version, tau) repeats and its gate chose the lane-per-site
+    kernel; every call equals a fresh engine's bit for bit, including after
+    the cost is changed in place (a new version: gated again)."""
+    B, n, L, Q = 2, 16, 700, 20
+    ch = random_topologies(B, n, seed=31)
+    lv = _dev(random_leaves(B, n, L, Q, seed=32, missing=0.01), device)
+    c = _dev(int_cost(Q, seed=33), device, torch.float32)
+    eng = _engine(ch, L, Q, device)
+
+    def fresh(cost):
+        f, dc, mg, _ = _engine(ch, L, Q, device).fwd_bwd(lv, cost.clone(), tau, marginals=True)
+        return f.tree_score, dc, mg
+
+    ref = fresh(c)
+    for i in range(4):
+        f, dc, mg, _ = eng.fwd_bwd(lv, c, tau, marginals=True)
+        assert torch.equal(f.tree_score, ref[0]) and torch.equal(dc, ref[1]), i
+        assert torch.equal(mg, ref[2]), i
+    if tau == 0.5 and wide_kernel == "wave":
+        assert eng._site_ok  # the third and fourth calls skipped the gate
+    c.mul_(2.0)
+    ref2 = fresh(c)
+    for i in range(3):
+        f, dc, mg, _ = eng.fwd_bwd(lv, c, tau, marginals=True)
+        assert torch.equal(f.tree_score, ref2[0]) and torch.equal(dc, ref2[1]), i
+        assert torch.equal(mg, ref2[2]), i

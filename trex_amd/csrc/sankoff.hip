@@ -1376,7 +1376,11 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
       float* kg = reinterpret_cast<float*>(tail - 3456);  // K and K^T
       c.site_flag = flag;
       c.site_kg = kg;
-      if (int e = wide_run(fn, c, /*reduce=*/false)) return e;
+      // TREX_FLAG_SITE_REUSE: an earlier call on this workspace with the same
+      // cost and tau left K, K^T and a set flag there (the caller read it):
+      // no gate launch
+      if (!(flags & TREX_FLAG_SITE_REUSE))
+        if (int e = wide_run(fn, c, /*reduce=*/false)) return e;
       if (int e = site_run(fn, c, lanes, lp_slots, flag, kg)) return e;
       return partial_reduce(fn, static_cast<double*>(workspace),
                             static_cast<double*>(workspace) + (int64_t)B * wide_tiles(L, Q), B,
@@ -1452,6 +1456,11 @@ using namespace trex;
 extern "C" const char* trex_last_error(void) { return g_err; }
 
 extern "C" int trex_version(void) { return 8; }
+
+extern "C" int64_t trex_site_flag_offset(int B, int L, int Q) {
+  if (B <= 0 || L <= 0 || Q <= 4 || Q > kWideMaxQ) return -1;
+  return wide_workspace_bytes(B, L, Q) - 128;
+}
 
 extern "C" int trex_dp_site_major(int Q) {
   (void)Q;
