@@ -2030,7 +2030,11 @@ __global__ __launch_bounds__(256) void adam_seq_update_kernel(
 // displace anything in L2 / MALL (C5: 329 -> 272 us, 4.9 -> 6.0 TB/s; two or
 // four rows per thread, or temporal accesses, were slower: DESIGN §9)
 typedef float fv4 __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void adam_seq_update4_kernel(
+#ifndef TREX_ADAM_BLOCK
+#define TREX_ADAM_BLOCK 256
+#endif
+constexpr int kAdamBlock = TREX_ADAM_BLOCK;  // threads per block of the Q = 4 ancestors' pass
+__global__ __launch_bounds__(kAdamBlock) void adam_seq_update4_kernel(
     const fv4* __restrict__ ds, int64_t rows, float T, float Tn, fv4* __restrict__ p,
     fv4* __restrict__ mu, fv4* __restrict__ nu, float lr, float b1, float b2, float eps,
     float bc1, float bc2, fv4* __restrict__ s_out, const StepState* __restrict__ ss) {
@@ -2040,7 +2044,7 @@ __global__ __launch_bounds__(256) void adam_seq_update4_kernel(
     T = ss->T;
     Tn = ss->Tn;
   }
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.x * kAdamBlock + threadIdx.x;
   if (r >= rows) return;
   const fv4 d = __builtin_nontemporal_load(ds + r), a = __builtin_nontemporal_load(p + r);
   const fv4 m = __builtin_nontemporal_load(mu + r), v = __builtin_nontemporal_load(nu + r);
@@ -2077,7 +2081,7 @@ __global__ __launch_bounds__(256) void split_x3_kernel(const float* __restrict__
 }
 
 // the Q = 4 ancestors' pass writing the next S rows pre-split (x3p)
-__global__ __launch_bounds__(256) void adam_seq_update4_x3p_kernel(
+__global__ __launch_bounds__(kAdamBlock) void adam_seq_update4_x3p_kernel(
     const fv4* __restrict__ ds, int64_t rows, float T, float Tn, fv4* __restrict__ p,
     fv4* __restrict__ mu, fv4* __restrict__ nu, float lr, float b1, float b2, float eps,
     float bc1, float bc2, float sx, fv4* __restrict__ s_out, const StepState* __restrict__ ss) {
@@ -2087,7 +2091,7 @@ __global__ __launch_bounds__(256) void adam_seq_update4_x3p_kernel(
     T = ss->T;
     Tn = ss->Tn;
   }
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = (int64_t)blockIdx.x * kAdamBlock + threadIdx.x;
   if (r >= rows) return;
   const fv4 d = __builtin_nontemporal_load(ds + r), a = __builtin_nontemporal_load(p + r);
   const fv4 m = __builtin_nontemporal_load(mu + r), v = __builtin_nontemporal_load(nu + r);
@@ -2114,7 +2118,7 @@ void launch_adam_seq(const float* ds, int64_t rows, int Q, float T, float Tn, fl
                     reinterpret_cast<uintptr_t>(mu) | reinterpret_cast<uintptr_t>(nu) |
                     reinterpret_cast<uintptr_t>(s_out)) & 15) == 0;
   if (Q == 4 && al && rows <= 0x7FFFFFFFLL * 256)
-    hipLaunchKernelGGL(adam_seq_update4_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(adam_seq_update4_kernel, dim3((unsigned)((rows + kAdamBlock - 1) / kAdamBlock)), dim3(kAdamBlock), 0,
                        st, reinterpret_cast<const fv4*>(ds), rows, T, Tn,
                        reinterpret_cast<fv4*>(p), reinterpret_cast<fv4*>(mu),
                        reinterpret_cast<fv4*>(nu), lr, b1, b2, eps, bc1, bc2,
@@ -2696,7 +2700,7 @@ extern "C" int trex_adam_seq_update_step_x3p(const float* ds_anc, int n_anc, int
   const int64_t rows = (int64_t)n_anc * L;
   const float bc1 = state ? 1.0f : bias_corr(b1, count);
   const float bc2 = state ? 1.0f : bias_corr(b2, count);
-  hipLaunchKernelGGL(adam_seq_update4_x3p_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256),
+  hipLaunchKernelGGL(adam_seq_update4_x3p_kernel, dim3((unsigned)((rows + kAdamBlock - 1) / kAdamBlock)), dim3(kAdamBlock),
                      0, (hipStream_t)stream, reinterpret_cast<const fv4*>(ds_anc), rows,
                      temperature, next_temperature, reinterpret_cast<fv4*>(params),
                      reinterpret_cast<fv4*>(mu), reinterpret_cast<fv4*>(nu), lr, b1, b2, eps, bc1,
