@@ -469,7 +469,8 @@ def c5_gemm_kernels(torch, opt):
     return out
 
 
-def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=256, L=50000):
+def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=256, L=50000,
+            dist_on=False):
     """C5 (BASELINE.json configs[4]): 256 taxa (511 nodes) x 50 000 sites x 4
     states, joint Adam optimisation step (update_seq, update_tree, surrogate
     + graph constraint, their VJPs, optax Adam) -- trex's
@@ -496,7 +497,8 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=25
               .contiguous()}
     noise = [gumbel_noise((n - 1, nl - 1), generator=g, device=device) for _ in range(4)]
     group = None
-    if world > 1:
+    dist_on = dist_on or world > 1
+    if dist_on:
         import torch.distributed as dist
 
         group = dist.group.WORLD
@@ -507,14 +509,14 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=25
     for k in range(warmup):
         opt.step(temp(k), noise[k % 4], next_temperature=temp(k + 1))
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(steps):
         loss = opt.step(temp(warmup + k), noise[k % 4], next_temperature=temp(warmup + k + 1))
     torch.cuda.synchronize()
     sec = (time.perf_counter() - t0) / steps
-    if world > 1:
+    if dist_on:
         t = torch.tensor([sec], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         sec = float(t.item())
@@ -530,11 +532,11 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=25
                  "size, tests/test_configs_full_gpu.py)" if opt.gemm == "x3" else "f32 MFMA GEMMs")
     res = {"workload": f"C5: {n}-node relaxed tree x {L} sites x {Q} states, joint Adam step "
                        "(surrogate + constraint + VJPs + optax adam), " + gemm_desc
-                       + (f"; sites sharded over {world} ranks, Gram all-reduce" if world > 1
+                       + (f"; sites sharded over {world} ranks, Gram all-reduce" if dist_on
                           else ""),
            "ms_per_step": sec * 1e3, "steps_per_s": 1.0 / sec, "n_gpus": world,
            "taxa": nl, "sites": L, "sites_rank0": hi - lo if rank == 0 else None,
-           "scaling": "strong" if world > 1 else None, "loss_last": float(loss),
+           "scaling": "strong" if dist_on else None, "loss_last": float(loss),
            "gemm": opt.gemm, "leaf_codes": opt.codes is not None,
            "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": step_bytes,
                         "achieved": round(step_bytes / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -671,9 +673,13 @@ def main():
     # TREX_BENCH_DEVICE_SHARE=1 rehearses N ranks on one GPU over gloo (code
     # path check only; timings are not meaningful); the driver's runs use RCCL
     share = os.environ.get("TREX_BENCH_DEVICE_SHARE") == "1"
+    # TREX_BENCH_FORCE_DIST=1 runs the N > 1 code path at N = 1 (RCCL
+    # process group, side-stream all-reduce, MAX timer): a one-GPU rehearsal
+    # of the backend the driver's 8-GPU run initialises
+    dist_on = world > 1 or os.environ.get("TREX_BENCH_FORCE_DIST") == "1"
     device = torch.device("cuda", 0 if share else local)
     torch.cuda.set_device(device)
-    if world > 1:
+    if dist_on:
         if share:
             dist.init_process_group("gloo")
         else:
@@ -703,7 +709,7 @@ def main():
     # overlaps the next step's kernel (double-buffered, as DDP overlaps its
     # gradient buckets with backward); every all-reduce completes inside the
     # timed region (synchronize at the end waits for both streams)
-    comm = torch.cuda.Stream(device) if world > 1 else None
+    comm = torch.cuda.Stream(device) if dist_on else None
     reds = [red, torch.zeros_like(red)]
     done = [torch.cuda.Event(), torch.cuda.Event()]
     it = [0]
@@ -713,7 +719,7 @@ def main():
             graph.replay()
         else:
             step()
-        if world > 1:
+        if dist_on:
             i = it[0] % 2
             it[0] += 1
             buf = reds[i]
@@ -729,17 +735,17 @@ def main():
     for _ in range(args.warmup):
         run_once()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run_once()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([el], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -752,7 +758,7 @@ def main():
         # the last step's reduced [dC (Q*Q), loss] (rank 0's copy after the
         # all-reduce; at N = 1 the step's own dC and loss): tests compare it
         # with the single-process engine over the whole batch
-        if world > 1:
+        if dist_on:
             last = reds[(it[0] - 1) % 2]
         else:
             last = torch.cat([step.out_b["d_cost"].view(-1),
@@ -810,12 +816,13 @@ def main():
                                f"{Q} states, softmin tau={tau} fwd (DP table written) + grad, "
                                f"split over {world} GPU(s) ({B} trees on rank 0)"
                                + ("; RCCL all-reduce of [dC, loss] per step, overlapped with "
-                                  "the next step" if world > 1 else ""),
+                                  "the next step" if dist_on else ""),
                    "trees": args.trees, "trees_rank0": B, "taxa": n, "sites": L, "states": Q,
-                   "tau": tau, "hipgraph": use_graph, "parallelism": f"tree-batch x{world}"},
+                   "tau": tau, "hipgraph": use_graph, "parallelism": f"tree-batch x{world}",
+                   "process_group": dist.get_backend() if dist_on else None},
         "roofline": roofline,
     }
-    if rank == 0 and world == 1:
+    if rank == 0 and not dist_on:
         hinfo, threads = host_cpu()
         threads = args.cpu_threads or threads
         if not args.no_cpu_baseline:
@@ -842,12 +849,13 @@ def main():
             result["nk"] = nk_line(torch, device)
         if not args.no_ragged:
             result["ragged"] = ragged_line(torch, device)
-    if world > 1 and not args.no_c5:
+    if dist_on and not args.no_c5:
         result["c5"] = c5_line(torch, device, steps=args.c5_steps, warmup=args.c5_warmup,
-                               rank=rank, world=world, nl=args.c5_taxa, L=args.c5_sites)
+                               rank=rank, world=world, nl=args.c5_taxa, L=args.c5_sites,
+                               dist_on=True)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -42,12 +42,10 @@ extern "C" {
 #define TREX_FLAG_HARD_ROOT 1u  /* tau>0: site score = min(D_root), not smin */
 /* 4 < Q <= 20 softmin: the lane-per-site kernel decides on the device, from
  * the cost matrix, whether it takes a call (a gate in the state-parallel
- * launch writes K, K^T and a flag into the workspace).  A caller that reused
- * the workspace with the same cost and tau and read that flag as set
- * (int32 at byte trex_site_flag_offset(B, L, Q) of the workspace) may pass
- * TREX_FLAG_SITE_REUSE: the gate launch is skipped.  Any other call on the
- * workspace may overwrite K and the flag. */
-#define TREX_FLAG_SITE_REUSE 2u
+ * launch writes K, K^T and a flag into the workspace tail on every call).
+ * Flag bit 2 (v8's TREX_FLAG_SITE_REUSE, which skipped that gate) is gone
+ * since v9 and refused with TREX_E_ARG: it saved no measurable time and
+ * trusted the caller to know when the cost changed. */
 
 /* plan layout constants (see trex_plan_build).  A plan holds, after the
  * header, the forward steps [B][n_int][4], the backtrack entries
@@ -57,6 +55,8 @@ extern "C" {
 
 const char* trex_last_error(void);
 /* ABI / plan-layout version.
+ * 9: TREX_FLAG_SITE_REUSE and trex_site_flag_offset removed (flags other
+ *    than TREX_FLAG_HARD_ROOT are refused).
  * 8: plan child descriptors may carry bit 28 and step words flag 8 (deferred
  *    cherry edges of the Q <= 4 adjoint; plans are passed through unchanged,
  *    so bindings are unaffected); trex_tree_surrogate_constraint and
@@ -74,7 +74,6 @@ const char* trex_last_error(void);
  *    v4 plans must re-query it), Q up to 64, ragged Q > 4.
  * 4: site-major DP tables. */
 int trex_version(void);
-int64_t trex_site_flag_offset(int B, int L, int Q); /* -1 when Q has no site kernel */
 
 /* ------------------------------------------------------------------------
  * Topology plan (host side; topology is static per call like trex's jit

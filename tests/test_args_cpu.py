@@ -37,6 +37,22 @@ def test_sankoff_rejects_bad_tau(tau):
     assert rc == TREX_E_ARG
 
 
+@pytest.mark.parametrize("Q", [4, 20])
+@pytest.mark.parametrize("flags", [2, 4, 0x80000000])
+def test_sankoff_rejects_unknown_flags(Q, flags):
+    """v9: only TREX_FLAG_HARD_ROOT is a flag (v8's TREX_FLAG_SITE_REUSE = 2
+    is refused, not silently ignored)."""
+    b = _buf()
+    p = b.ctypes.data
+    L = lib()
+    ws = int(L.trex_workspace_bytes(1, 64, 7, Q))
+    w = _buf(ws)
+    rc = L.trex_sankoff_fwd(p, 2, p, p, 1, 64, 7, Q, 0.5, flags, p, None, p, w.ctypes.data, ws,
+                            None)
+    assert rc == TREX_E_ARG, (flags, rc)
+    assert b"flags" in L.trex_last_error()
+
+
 @pytest.mark.parametrize("bad", [float("nan"), float("inf"), 0.0, -2.0])
 def test_split_gemms_reject_bad_bounds(bad):
     b = _buf()

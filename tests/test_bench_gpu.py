@@ -110,3 +110,50 @@ def test_bench_world2_c5_site_shard_matches_single_process():
                            L=sites)
     assert single["n_gpus"] == 1
     np.testing.assert_allclose(c5["loss_last"], single["loss_last"], rtol=1e-5)
+
+
+def test_bench_rccl_one_rank_rehearsal(tmp_path):
+    """bench.py's N > 1 code path with a real RCCL
+    process group ("nccl" on ROCm), forced at world 1 (TREX_BENCH_FORCE_DIST)
+    because this box has one GPU: init_process_group("nccl", device_id=...),
+    the side-stream all-reduce of [dC, loss] overlapped with the next step,
+    the barriers and the MAX-reduced timer, then the C5 leg's Gram all-reduce
+    (TreeOptimizer(group=WORLD)).  A one-rank all-reduce is the identity, so
+    the dumped [dC, loss] equals the engine's own over the same batch bit for
+    bit, and the C5 loss equals the single-process leg's."""
+    trees, taxa, sites, states, steps = 32, 16, 700, 4, 3
+    dump = tmp_path / "reduced.npy"
+    env = dict(os.environ, TREX_BENCH_FORCE_DIST="1", TREX_BENCH_DUMP=str(dump))
+    env.pop("TREX_BENCH_DEVICE_SHARE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "1", "--steps", str(steps), "--warmup", "1", "--trees", str(trees),
+           "--taxa", str(taxa), "--sites", str(sites), "--states", str(states),
+           "--c5-taxa", "64", "--c5-sites", "300", "--c5-steps", "3", "--c5-warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 1 and res["config"]["process_group"] == "nccl"
+    assert "RCCL all-reduce" in res["config"]["workload"]
+    assert res["c5"]["scaling"] == "strong" and res["c5"]["n_gpus"] == 1
+
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    from trex_amd import SankoffEngine
+
+    dev = torch.device("cuda", 0)
+    ch, plan, leaves, cost = bench.make_inputs(torch, dev, trees, taxa, sites, states, 0, trees)
+    eng = SankoffEngine(plan, sites, states, dev)
+    f, dc, _, _ = eng.fwd_bwd(leaves, cost, 0.5)
+    torch.cuda.synchronize()
+    red = np.load(dump)
+    q2 = states * states
+    np.testing.assert_array_equal(red[:q2].reshape(states, states), dc.cpu().numpy())
+    assert red[q2] == np.float32(f.tree_score.sum().item())
+    single = bench.c5_line(torch, dev, steps=3, warmup=1, nl=64, L=300)
+    np.testing.assert_allclose(res["c5"]["loss_last"], single["loss_last"], rtol=1e-6)

@@ -270,11 +270,11 @@ def test_c3_scale_properties(device):
 
 
 @pytest.mark.parametrize("tau", [0.5, 0.02])  # 0.02: range / tau > 40, the gate refuses
-def test_site_gate_reuse_is_bitwise_neutral(device, tau, wide_kernel):
-    """SankoffEngine passes TREX_FLAG_SITE_REUSE (no gate launch) once a
-    (cost tensor, version, tau) repeats and its gate chose the lane-per-site
-    kernel; every call equals a fresh engine's bit for bit, including after
-    the cost is changed in place (a new version: gated again)."""
+def test_site_gate_repeat_calls_no_sync(device, tau, wide_kernel):
+    """Every call runs the lane-per-site gate (v8's TREX_FLAG_SITE_REUSE is
+    gone): repeated eager calls on one engine equal a fresh engine's bit for
+    bit, including after the cost is changed in place, and none of them
+    synchronises with the host (torch's sync debug mode raises on any)."""
     B, n, L, Q = 2, 16, 700, 20
     ch = random_topologies(B, n, seed=31)
     lv = _dev(random_leaves(B, n, L, Q, seed=32, missing=0.01), device)
@@ -286,12 +286,19 @@ def test_site_gate_reuse_is_bitwise_neutral(device, tau, wide_kernel):
         return f.tree_score, dc, mg
 
     ref = fresh(c)
-    for i in range(4):
-        f, dc, mg, _ = eng.fwd_bwd(lv, c, tau, marginals=True)
-        assert torch.equal(f.tree_score, ref[0]) and torch.equal(dc, ref[1]), i
-        assert torch.equal(mg, ref[2]), i
-    if tau == 0.5 and wide_kernel == "wave":
-        assert eng._site_ok  # the third and fourth calls skipped the gate
+    outs = {"dp": torch.empty(eng.dp_shape, device=device),
+            "marginals": torch.empty(eng.dp_shape, device=device),
+            "tree_score": torch.empty(B, device=device),
+            "d_cost": torch.empty(Q, Q, device=device)}
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        for _ in range(10):
+            eng.fwd_bwd(lv, c, tau, marginals=True, out=outs)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    assert torch.equal(outs["tree_score"], ref[0]) and torch.equal(outs["d_cost"], ref[1])
+    assert torch.equal(outs["marginals"], ref[2])
     c.mul_(2.0)
     ref2 = fresh(c)
     for i in range(3):

@@ -726,6 +726,69 @@ def test_tree_device_loop_after_more_eager_steps(device):
         assert torch.equal(dut.params[k], ref.params[k]), k
 
 
+@pytest.mark.parametrize("gemm", ["x3", "f32"])
+def test_tree_device_loop_after_load_checkpoint(device, gemm, tmp_path):
+    """a captured loop replays with S's (S16's) ancestor rows as
+    the previous replay left them.  Load an earlier checkpoint into the
+    looping optimiser, and then take an eager step whose next temperature
+    leaves the schedule: each time run() must first refresh the rows, so
+    the replays stay bitwise an uninterrupted eager run from that state."""
+    params, _, seqs = _tree_case(16, 52, 4, 37)
+    temps = [max(0.1, 2.0 * (1.0 - k / 40)) for k in range(16)]
+    seed = 7
+
+    def make():
+        return G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                               lr=0.02, gemm=gemm)
+
+    shape = None
+
+    def eager(o, k, t_next=None):
+        return float(o.step(temps[k - 1], G.gumbel_noise_step(seed, k, shape, device),
+                            temps[k] if t_next is None else t_next))
+
+    ref = make()
+    shape = (ref.N - 1, ref.n_anc)
+    dut = make()
+    loop = dut.device_loop(temps, seed, capture=True)
+    loop.run(2)
+    path = tmp_path / "c5.npz"
+    dut.save_checkpoint(path)  # after step 2
+    loop.run(3)  # steps 3..5: the rows now belong to step 6
+    dut.load_checkpoint(path)  # back to step 2's state
+    for k in (1, 2):
+        eager(ref, k)
+    for k in (3, 4):
+        assert float(loop.run(1)) == eager(ref, k), k
+    # an eager step announcing a temperature off the schedule
+    assert eager(dut, 5, 0.77) == eager(ref, 5, 0.77)
+    for k in (6, 7):
+        assert float(loop.run(1)) == eager(ref, k), k
+    torch.cuda.synchronize()
+    for k in ref.params:
+        assert torch.equal(dut.params[k], ref.params[k]), k
+
+
+def test_tree_optimizer_sequences_accessor(device, monkeypatch):
+    """TreeOptimizer.sequences(): the current softmaxes in every mode.  In
+    pre-split mode S's ancestor rows go stale (only S16's are kept); the
+    accessor recomputes them, equal bit for bit to the f32-operand mode's S."""
+    params, noise, seqs = _tree_case(16, 52, 4, 43)
+    nz = _t(noise, device)
+    temps = [1.5, 1.2, 1.0, 0.8]
+    got = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TREX_PRESPLIT", flag)
+        opt = G.TreeOptimizer(_t(seqs, device), {k: _t(v, device) for k, v in params.items()},
+                              lr=0.02)
+        for i in range(3):
+            opt.step(temps[i], nz, temps[i + 1])
+        got.append(opt.sequences())
+        if flag == "0":
+            assert torch.equal(got[-1], opt.S)
+    assert torch.equal(got[0], got[1])
+
+
 @pytest.mark.parametrize("nl,L,loop", [(100, 50, False), (256, 1001, False), (16, 52, True),
                                        (40, 33, False)])
 def test_tree_optimizer_presplit_operands_are_bitwise_neutral(device, monkeypatch, nl, L, loop):

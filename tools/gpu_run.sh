@@ -1,0 +1,61 @@
+#!/bin/bash
+# One gpurun call made of named steps; every GPU step runs under its own time
+# limit and the first failure ends the call (no further GPU step after it).
+#
+# usage (from the repo root, on the GPU box):
+#   tools/gpu_run.sh TAG STEP [STEP ...]
+# steps (arguments after ':' are comma-separated, commas become spaces):
+#   suite[:paths]   pytest -m gpu over tests/ (or the paths) -> TAG_suite.log
+#   smoke           __graft_entry__.smoke()                  -> TAG_smoke.log
+#   bench[:args]    python bench.py args                     -> TAG_bench.json
+#   prof[:args]     rocprofv3 --kernel-trace --stats of bench.py args
+#                   -> TAG_prof/ (+ TAG_prof_by_grid.txt)
+#   pmc:file        tools/pmc_passes.sh style counter passes listed in file
+#   ab_libs:a.so,b.so   tools/ab_libs.sh over those libraries -> TAG_ab.txt
+#   ab_env:A=1,A=0      tools/ab_env.sh over those settings    -> TAG_ab.txt
+# outputs land in gpurun_out/TAG_*.
+set -o pipefail
+TAG=$1
+shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for step in "$@"; do
+  name=${step%%:*}
+  arg=""
+  [[ "$step" == *:* ]] && arg=$(echo "${step#*:}" | tr ',' ' ')
+  echo "[gpu_run] $TAG $name $arg"
+  case "$name" in
+    suite)
+      timeout -k 10 900 python -u -m pytest ${arg:-tests} -m gpu -x -q --timeout 120 \
+        --timeout-method thread > "$OUT/${TAG}_suite.log" 2>&1 || { tail -30 "$OUT/${TAG}_suite.log"; exit 1; }
+      tail -3 "$OUT/${TAG}_suite.log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" \
+        > "$OUT/${TAG}_smoke.log" 2>&1 || { cat "$OUT/${TAG}_smoke.log"; exit 1; } ;;
+    bench)
+      timeout -k 10 600 python -u bench.py $arg > "$OUT/${TAG}_bench.json" \
+        2> "$OUT/${TAG}_bench.err" || { tail -30 "$OUT/${TAG}_bench.err"; exit 1; }
+      tail -c 600 "$OUT/${TAG}_bench.json" ;;
+    prof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run \
+        --output-format csv -- python3 "$ROOT/bench.py" $arg > "$OUT/${TAG}_prof_bench.json" \
+        2> "$OUT/${TAG}_prof.err") || { tail -30 "$OUT/${TAG}_prof.err"; exit 1; }
+      for csv in $(find "$OUT/${TAG}_prof" -name '*kernel_trace.csv'); do
+        python3 "$ROOT/tools/kernels_by_grid.py" "$csv" >> "$OUT/${TAG}_prof_by_grid.txt" 2>&1
+      done
+      cat "$OUT/${TAG}_prof_by_grid.txt" ;;
+    ab_libs)
+      timeout -k 10 900 bash "$ROOT/tools/ab_libs.sh" $arg > "$OUT/${TAG}_ab.txt" 2>&1 \
+        || { tail -30 "$OUT/${TAG}_ab.txt"; exit 1; }
+      cat "$OUT/${TAG}_ab.txt" | tail -20 ;;
+    ab_env)
+      timeout -k 10 900 bash "$ROOT/tools/ab_env.sh" $arg ${REPS:-2} > "$OUT/${TAG}_ab.txt" 2>&1 \
+        || { tail -30 "$OUT/${TAG}_ab.txt"; exit 1; }
+      cat "$OUT/${TAG}_ab.txt" | tail -20 ;;
+    *)
+      echo "unknown step $name"; exit 2 ;;
+  esac
+done
+echo "[gpu_run] $TAG done"

@@ -20,7 +20,6 @@ TREX_E_TOPOLOGY = -2
 TREX_E_UNSUPPORTED = -3
 TREX_E_HIP = -4
 TREX_FLAG_HARD_ROOT = 1
-TREX_FLAG_SITE_REUSE = 2
 TREX_PLAN_HEADER_INTS = 16
 
 _c_i = ctypes.c_int
@@ -33,7 +32,6 @@ _p = ctypes.c_void_p
 SIGNATURES = {
     "trex_last_error": (ctypes.c_char_p, []),
     "trex_version": (_c_i, []),
-    "trex_site_flag_offset": (_c_i64, [_c_i, _c_i, _c_i]),
     "trex_plan_ints": (_c_i64, [_c_i, _c_i]),
     "trex_plan_build": (_c_i, [_p, _c_i, _c_i, _p, _p]),
     "trex_workspace_bytes": (_c_i64, [_c_i, _c_i, _c_i, _c_i]),

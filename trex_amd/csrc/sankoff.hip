@@ -1332,6 +1332,7 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
   if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
   if (n_slots < 0) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  if (flags & ~TREX_FLAG_HARD_ROOT) return set_error(TREX_E_ARG, "%s: unknown flags 0x%x", fn, flags);
   // plan info[0]: stack depth | (lane-program slots + 1) << 16
   const int lp_slots = ((n_slots >> 16) & 0xFF) - 1;
   n_slots &= 0xFFFF;
@@ -1376,11 +1377,7 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
       float* kg = reinterpret_cast<float*>(tail - 3456);  // K and K^T
       c.site_flag = flag;
       c.site_kg = kg;
-      // TREX_FLAG_SITE_REUSE: an earlier call on this workspace with the same
-      // cost and tau left K, K^T and a set flag there (the caller read it):
-      // no gate launch
-      if (!(flags & TREX_FLAG_SITE_REUSE))
-        if (int e = wide_run(fn, c, /*reduce=*/false)) return e;
+      if (int e = wide_run(fn, c, /*reduce=*/false)) return e;
       if (int e = site_run(fn, c, lanes, lp_slots, flag, kg)) return e;
       return partial_reduce(fn, static_cast<double*>(workspace),
                             static_cast<double*>(workspace) + (int64_t)B * wide_tiles(L, Q), B,
@@ -1455,12 +1452,7 @@ using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 8; }
-
-extern "C" int64_t trex_site_flag_offset(int B, int L, int Q) {
-  if (B <= 0 || L <= 0 || Q <= 4 || Q > kWideMaxQ) return -1;
-  return wide_workspace_bytes(B, L, Q) - 128;
-}
+extern "C" int trex_version(void) { return 9; }
 
 extern "C" int trex_dp_site_major(int Q) {
   (void)Q;
@@ -1586,6 +1578,7 @@ extern "C" int trex_sankoff_ragged(int phase, const int32_t* plan, int B, int n_
   if (workspace_bytes < trex_ragged_workspace_bytes(items, Q))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
   if (n_slots < 0 || n_slots > 250) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
+  if (flags & ~TREX_FLAG_HARD_ROOT) return set_error(TREX_E_ARG, "%s: unknown flags 0x%x", fn, flags);
   if (Q > 4) {
     // protein / codon alphabets: the state-parallel kernel, each 64-site
     // item split over ceil(64 / sites-per-wave) waves

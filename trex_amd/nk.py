@@ -152,10 +152,15 @@ class LandscapeAwareLoss:
         nb = int(L_.trex_nk_workspace_bytes(self.N, self.L, self.Q, k, self.n_parents))
         self.nk_ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)
 
-    def value_and_grad(self, ancestors, masked_sequences, *, want_grad: bool = True, out=None):
+    def value_and_grad(self, ancestors, masked_sequences, *, want_grad: bool = True, out=None,
+                       refresh: bool = False):
         """(loss (1,) device tensor, d loss / d ancestors (n_anc, L, Q)).
         ``out``: a preallocated (n_anc, L, Q) gradient buffer (no allocation:
-        the call launches only kernels and is hipGraph-capturable)."""
+        the call launches only kernels and is hipGraph-capturable).
+        ``masked_sequences`` is copied only when it is another tensor than
+        last call's or torch's version counter moved; a write through a raw
+        pointer (a trex_* kernel, DLPack) is invisible to that counter, so
+        pass ``refresh=True`` after one."""
         torch = _torch()
         L_ = lib()
         dev = self.S.device
@@ -164,7 +169,7 @@ class LandscapeAwareLoss:
         n_anc = self.N - self.n_leaves
         if tuple(anc.shape) != (n_anc, self.L, self.Q):
             raise ValueError(f"ancestors must be {(n_anc, self.L, self.Q)}")
-        self._set_leaves(masked_sequences)
+        self._set_leaves(masked_sequences, refresh)
         check(L_.trex_tree_update_seq(ptr(anc), n_anc, self.L, self.Q, self.T,
                                       ptr(self.S[self.n_leaves:]), st))
         dS = self._loss_and_dS(want_grad)
@@ -175,14 +180,14 @@ class LandscapeAwareLoss:
                                           n_anc, self.L, self.Q, self.T, ptr(d_anc), st))
         return self.loss, d_anc
 
-    def _set_leaves(self, masked_sequences):
+    def _set_leaves(self, masked_sequences, refresh=False):
         # S = masked_sequences with the ancestor rows rewritten: the copy is
         # needed only when the caller passes another tensor or wrote into
         # this one (torch's version counter); the cached reference keeps the
         # tensor alive, so its storage cannot be reused under the cache
         ms = _f32(masked_sequences, self.S.device)
         ver = getattr(ms, "_version", None)
-        if ms is not self._s_src or ver is None or ver != self._s_ver:
+        if refresh or ms is not self._s_src or ver is None or ver != self._s_ver:
             self.S.copy_(ms)
             self._s_src, self._s_ver = ms, ver
 

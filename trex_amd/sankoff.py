@@ -13,13 +13,11 @@ device memory and streams.  There is no CPU fallback.
 
 from __future__ import annotations
 
-import weakref
-
 from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import TREX_FLAG_HARD_ROOT, TREX_FLAG_SITE_REUSE, check, lib, ptr, stream_handle
+from ._lib import TREX_FLAG_HARD_ROOT, check, lib, ptr, stream_handle
 from .topology import TreePlan, children_from_adjacency
 
 SENTINEL = 1e5  # src/trex/sankoff.py:152
@@ -83,43 +81,10 @@ class SankoffEngine:
         self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         # arrival counters of the in-kernel reductions start at zero
         check(lib().trex_workspace_init(ptr(self.workspace), nbytes, stream_handle(self.device)))
-        # 4 < Q <= 20 softmin: where the lane-per-site kernel's gate leaves
-        # its flag in the workspace (TREX_FLAG_SITE_REUSE, include/trex_hip.h)
-        self._site_flag_at = int(lib().trex_site_flag_offset(plan.B, self.L, self.Q))
-        self._site_ref = self._site_key = None  # last (cost, (version, tau)) gated
-        self._site_ok = False  # ... and its gate chose the lane-per-site kernel
 
-    def _flags(self, cost, tau, hard_root):
-        """Call flags; TREX_FLAG_SITE_REUSE when earlier calls on this
-        workspace ran the site gate on the same cost tensor (identity, held
-        weakly, and version) and tau and the gate chose the lane-per-site
-        kernel.  Returns (flags, whether to read the gate's flag after this
-        call): the flag is read (a host sync) only when a (cost, tau) repeats,
-        so a loop that changes the cost every call never synchronises."""
-        flags = TREX_FLAG_HARD_ROOT if hard_root else 0
-        torch = _torch()
-        if torch.cuda.is_current_stream_capturing():
-            # a captured graph keeps its gate: it must not depend on what
-            # eager calls leave in the workspace between replays
-            return flags, False
-        if self._site_flag_at < 0 or not tau > 0:
-            self._site_key = None
-            return flags, False
-        key = (cost._version, float(tau))
-        same = self._site_ref is not None and self._site_ref() is cost and self._site_key == key
-        if same and self._site_ok:
-            return flags | TREX_FLAG_SITE_REUSE, False
-        self._site_ref, self._site_key, self._site_ok = weakref.ref(cost), key, False
-        return flags, same
-
-    def _after(self, read):
-        """After an eager call that ran the gate on a repeated (cost, tau):
-        read the gate's flag."""
-        torch = _torch()
-        if not read:
-            return
-        at = self._site_flag_at
-        self._site_ok = int(self.workspace[at:at + 4].view(torch.int32).item()) == 1
+    @staticmethod
+    def _flags(hard_root):
+        return TREX_FLAG_HARD_ROOT if hard_root else 0
 
     # -- shapes ------------------------------------------------------------
     @property
@@ -175,12 +140,11 @@ class SankoffEngine:
         ts = o.get("tree_score")
         if ts is None:
             ts = torch.empty((p.B,), dtype=torch.float32, device=self.device)
-        flags, read = self._flags(cost, tau, hard_root)
+        flags = self._flags(hard_root)
         check(lib().trex_sankoff_fwd(
             ptr(self.plan_dev), p.slot_word, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
             self.Q, float(tau), flags, ptr(dp_t), ptr(ss), ptr(ts), ptr(self.workspace),
             self.workspace.numel(), stream_handle(self.device)))
-        self._after(read)
         return ForwardResult(ts, dp_t, ss)
 
     def backward(self, leaves, cost, tau: float, dp, d_tree_score=None, *, marginals=False,
@@ -208,12 +172,11 @@ class SankoffEngine:
                                            device=self.device).contiguous()
             if d_tree_score.shape != (p.B,):
                 raise ValueError("d_tree_score must be (B,)")
-        flags, read = self._flags(cost, tau, hard_root)
+        flags = self._flags(hard_root)
         check(lib().trex_sankoff_bwd(
             ptr(self.plan_dev), p.slot_word, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
             self.Q, float(tau), flags, ptr(dp), ptr(d_tree_score), ptr(dc), ptr(mg), ptr(an),
             ptr(self.workspace), self.workspace.numel(), stream_handle(self.device)))
-        self._after(read)
         return dc, mg, an
 
     def fwd_bwd(self, leaves, cost, tau: float = 0.0, d_tree_score=None, *, site_score=False,
@@ -246,13 +209,12 @@ class SankoffEngine:
                                            device=self.device).contiguous()
             if d_tree_score.shape != (p.B,):
                 raise ValueError("d_tree_score must be (B,)")
-        flags, read = self._flags(cost, tau, hard_root)
+        flags = self._flags(hard_root)
         check(lib().trex_sankoff_fwd_bwd(
             ptr(self.plan_dev), p.slot_word, ptr(leaves), ptr(cost), p.B, self.L, p.n_all,
             self.Q, float(tau), flags, ptr(dp_t), ptr(ss), ptr(ts), ptr(d_tree_score), ptr(dc),
             ptr(mg), ptr(an), ptr(self.workspace), self.workspace.numel(),
             stream_handle(self.device)))
-        self._after(read)
         return ForwardResult(ts, dp_t, ss), dc, mg, an
 
     def backtrack(self, cost, dp):

@@ -389,7 +389,11 @@ class TreeOptimizer:
                  graph_constraint_scale: float = 10.0, clip_norm=None, group=None,
                  gemm: str = "x3"):
         torch = _torch()
-        self.S = _dev(sequences).clone()  # (N, L, Q): leaf rows fixed, ancestors overwritten
+        # (N, L, Q): leaf rows fixed, ancestor rows rewritten by each step --
+        # except in pre-split mode (x3, Q = 4, no clipping), where the steps
+        # keep only S16's ancestor rows current and S's go stale after the
+        # first step: read sequences() for the current softmaxes
+        self.S = _dev(sequences).clone()
         dev = self.S.device
         self.params = {"tree_params": _dev(params["tree_params"], dev).clone(),
                        "ancestors": _ancestors(params).to(dev).clone()}
@@ -469,6 +473,20 @@ class TreeOptimizer:
             self.M16 = torch.zeros((self.N, self.ldm), **f32)
             check(lib().trex_tree_split_x3(ptr(self.S), self.N, self.K, self.K, 1.0,
                                            ptr(self.S16), self.K, stream_handle(dev)))
+
+    def sequences(self, temperature=None):
+        """S with its ancestor rows recomputed from the current ancestor
+        logits (update_seq at ``temperature``; default: the temperature the
+        next step will use) -- a fresh (N, L, Q) tensor, valid in every mode
+        (``self.S``'s ancestor rows are not, in pre-split mode)."""
+        T = self._s_temperature if temperature is None else float(temperature)
+        if T is None:
+            raise ValueError("sequences(): no step has fixed a temperature yet; pass one")
+        out = self.S.clone()
+        check(lib().trex_tree_update_seq(ptr(self.params["ancestors"]), self.n_anc, self.L,
+                                         self.Q, T, ptr(out[self.n_leaf:]),
+                                         stream_handle(self.S.device)))
+        return out
 
     def _split_anc(self, st):
         """S16's ancestor rows from S's (after update_seq rewrote them)."""
@@ -669,20 +687,29 @@ class _TreeDeviceLoop:
         k0 = opt.opt.count  # steps taken so far
         if k0 >= self.n_temps:
             raise ValueError("temperatures must cover the next step")
-        T0 = self.host_temps[k0]
-        if opt._s_temperature != T0:  # S rows at the first step's temperature
-            check(lib().trex_tree_update_seq(ptr(opt.params["ancestors"]), opt.n_anc, opt.L,
-                                             opt.Q, T0, ptr(opt.S[opt.n_leaf:]),
-                                             stream_handle(dev)))
-            if opt.presplit:
-                opt._split_anc(stream_handle(dev))
-            opt._s_temperature = T0
+        self._refresh_rows()
         if capture:
             # capture records launches without running them: the state
             # advances only on replays
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._launch()
+
+    def _refresh_rows(self):
+        """The ancestor rows of S (S16 when pre-split) at the next step's
+        temperature.  A captured step reads them as the previous replay left
+        them, so anything that replaced them in between -- load_state_dict /
+        load_checkpoint, an eager step() with another next temperature --
+        must be caught up eagerly before the next replay."""
+        o = self.opt
+        T = self.host_temps[o.opt.count]
+        if o._s_temperature != T:
+            st = stream_handle(o.S.device)
+            check(lib().trex_tree_update_seq(ptr(o.params["ancestors"]), o.n_anc, o.L, o.Q, T,
+                                             ptr(o.S[o.n_leaf:]), st))
+            if o.presplit:
+                o._split_anc(st)
+            o._s_temperature = T
 
     def _launch(self):
         o = self.opt
@@ -724,6 +751,8 @@ class _TreeDeviceLoop:
         if o.opt.count + n_steps > self.n_temps:
             raise ValueError("the temperature schedule does not cover these steps")
         o.opt.sync_state()  # eager steps since the capture counted on the host
+        if n_steps > 0:
+            self._refresh_rows()
         for _ in range(int(n_steps)):
             if self.graph is not None:
                 self.graph.replay()
