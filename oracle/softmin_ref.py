@@ -90,7 +90,18 @@ def sankoff_fwd_bwd_ref(children, leaves, cost, tau, d_tree_score=1.0,
 
     children (n_all, 2) int; leaves (n_leaves, L) int8 codes (-1 = missing);
     cost (Q, Q).  Returns dict with dp (n_int, Q, L), site_score (L,),
-    tree_score, d_cost (Q, Q), marginals (n_int, Q, L).
+    tree_score, d_cost (Q, Q), marginals (n_int, Q, L), and dp_mag
+    (n_int, Q, L), each D entry's error scale for an fp32 evaluation:
+
+        Dmag_v[i] = sum_c (|C_ij*| + tau log s_c[i] + Dmag_c*),
+
+    j* = argmin_j (C_ij + D_c[j]), s_c[i] = sum_j exp(-(x_j - min x) / tau),
+    Dmag_c* = sum_j w_c[i, j] Dmag_c[j] for an internal child, |D_c[j*]| for
+    a leaf / 1e5 row (exact inputs; 1e5 for a missing state).  This is the
+    running error bound of the recursion -- D evaluated with every term's
+    magnitude (M_c[i] = C_ij* + D_c[j*] - tau log s_c[i]; a softmin is
+    1-Lipschitz, so the child's error arrives weighted by w).  A D entry that
+    sums messages of either sign to ~0 keeps the absolute scale of its terms.
     """
     cost = np.asarray(cost, dtype=np.float64)
     Q = cost.shape[0]
@@ -101,12 +112,24 @@ def sankoff_fwd_bwd_ref(children, leaves, cost, tau, d_tree_score=1.0,
     leafD = leaf_dp(leaves[:n_leaves], Q)  # (n_leaves, L, Q)
     kinds = classify_children(children, n_all)
     D = np.zeros((n_int, L, Q))
+    Dmag = np.zeros((n_int, L, Q))  # error scale of D (docstring)
     for r in range(n_int):
         acc = np.zeros((L, Q))
+        mag = np.zeros((L, Q))
         for kind, idx in kinds[r]:
             x = _child_x(kind, idx, cost, leafD, D)
-            acc = acc + _smin(x, tau)[0]
+            M, w = _smin(x, tau)
+            acc = acc + M
+            js = np.argmin(x, axis=-1)  # (L, Qi)
+            xm = np.take_along_axis(x, js[..., None], axis=-1)[..., 0]
+            mag = mag + np.abs(cost[np.arange(Q)[None, :], js]) + (xm - M)  # xm - M = tau log s
+            if kind == "int":
+                mag = mag + np.einsum("lij,lj->li", w, Dmag[idx])
+            else:
+                dcs = np.take_along_axis(x - cost[None, :, :], js[..., None], axis=-1)[..., 0]
+                mag = mag + np.abs(dcs)
         D[r] = acc
+        Dmag[r] = mag
     Droot = D[n_int - 1]
     site, groot = _smin(Droot, 0.0 if hard_root else tau)
     # adjoint, reverse node order (children have lower indices)
@@ -126,6 +149,7 @@ def sankoff_fwd_bwd_ref(children, leaves, cost, tau, d_tree_score=1.0,
                 G[idx] += contrib.sum(axis=1)
     return {
         "dp": D.transpose(0, 2, 1).copy(),
+        "dp_mag": Dmag.transpose(0, 2, 1).copy(),
         "site_score": site,
         "tree_score": site.sum(),
         "d_cost": dC,
@@ -143,6 +167,7 @@ def batched_fwd_bwd_ref(children, leaves, cost, tau, d_tree_score=None,
                                 float(d_tree_score[b]), hard_root) for b in range(B)]
     return {
         "dp": np.stack([o["dp"] for o in outs]),
+        "dp_mag": np.stack([o["dp_mag"] for o in outs]),
         "site_score": np.stack([o["site_score"] for o in outs]),
         "tree_score": np.array([o["tree_score"] for o in outs]),
         "d_cost": sum(o["d_cost"] for o in outs),

@@ -151,6 +151,15 @@ def assert_bound_close(got, ref, bound, what="value"):
     return float(ratio[k])
 
 
+def assert_dp_close(got, ref, rtol=1e-5, what="dp"):
+    """Softmin DP table vs the fp64 oracle, per entry: |got - ref| <= rtol *
+    dp_mag (oracle/softmin_ref.py: the running error bound of the recursion,
+    every term of every message at its magnitude -- a D entry summing
+    messages of either sign keeps their absolute scale) + 1e-30.  got / ref in
+    the oracle's (B, n_int, Q, L) order.  Returns the max err / bound."""
+    return assert_bound_close(got, ref["dp"], rtol * ref["dp_mag"] + 1e-30, what=what)
+
+
 def path_dmax(children, dp_ref):
     """Per (tree, internal row, site): the sum over the row and its ancestors
     (root included) of max_state |D|.  children (B, n_all, 2) trex child ids;
@@ -233,7 +242,102 @@ def surrogate_grad_bounds(S, A, rtol=1e-5, constraint_grad=None):
     return bS.reshape(S.shape), rtol * bA
 
 
+def softmax_vjp_bound(P, M, axis=-1):
+    """Magnitude bound of a softmax VJP P (g - sum(P g)) for |g| <= M
+    (elementwise): P (M + sum(P M))."""
+    return P * (M + np.sum(P * M, axis=axis, keepdims=True))
+
+
+EPS_VJP = 8 * 2.0 ** -24  # a few fp32 roundings of the VJP's own arithmetic
+
+
+def tree_param_select(dz, n_anc):
+    """update_tree_vjp's map from the (n, n) logit cotangent to tree_params
+    (oracle/tree_ref.py:73-78; tree.py:63-105 masking), temperature 1."""
+    n = dz.shape[0]
+    nl = n - n_anc
+    dp = np.zeros((n - 1, n_anc))
+    dp[:nl] = dz[:nl, nl:]
+    i = np.arange(n_anc - 1)[:, None]
+    j = np.arange(n_anc)[None, :]
+    dp[nl:] = np.where(j > i, dz[nl:-1, nl:], 0.0)
+    return dp
+
+
+def loss_grad_bounds(noise, params, sequences, temperature, adjacency=None, *, rtol=1e-5,
+                     fix_seqs=False, fix_tree=False, scale=10.0):
+    """Per-entry bounds for compute_loss's gradients (tree.py:299-342; the
+    oracle's compute_loss): dA / dS at rtol times their terms' magnitudes
+    (surrogate_grad_bounds), carried through each softmax VJP (update_tree's
+    rows, update_seq's states: softmax_vjp_bound) plus that VJP's own
+    rounding at the magnitude of the exact cotangent.  Returns
+    {tree_params, ancestors} bound arrays."""
+    from oracle import tree_ref as T
+
+    anc = np.asarray(params["ancestors"], dtype=np.float64)
+    theta = np.asarray(params["tree_params"], dtype=np.float64)
+    S = sequences if fix_seqs else T.update_seq(anc, sequences, temperature)
+    A = adjacency if fix_tree else T.update_tree(theta, noise, 1.0)
+    S = np.asarray(S, dtype=np.float64)
+    A = np.asarray(A, dtype=np.float64)
+    _, dS, dA = T.compute_surrogate_cost_grads(S, A)
+    cg = temperature * T.enforce_graph_constraints_grad(A, scale)
+    dA = dA + cg
+    bS, bA = surrogate_grad_bounds(S, A, rtol, constraint_grad=cg)
+    out = {"tree_params": np.zeros_like(theta), "ancestors": np.zeros_like(anc)}
+    if not fix_tree:
+        dz = softmax_vjp_bound(A, bA, axis=1) + EPS_VJP * softmax_vjp_bound(A, np.abs(dA), axis=1)
+        out["tree_params"] = tree_param_select(dz, theta.shape[1])
+    if not fix_seqs:
+        nl = (S.shape[0] + 1) // 2
+        Sa = S[nl:]
+        out["ancestors"] = temperature * (softmax_vjp_bound(Sa, bS[nl:])
+                                          + EPS_VJP * softmax_vjp_bound(Sa, np.abs(dS[nl:])))
+    return out
+
+
+def landscape_grad_bound(ancestors, masked_sequences, n_leaves, interactions, fitness, adj,
+                         lambda_val, real_k, temperature=1.0, seq_mask=None, rtol=1e-5):
+    """Per-entry bound for d loss / d ancestors of the NK landscape-aware
+    loss (benchmark.py:235-306; oracle/nk_ref.py): every term of d loss / dS
+    at its magnitude -- the surrogate's (surrogate_grad_bounds), the child
+    cross-entropy's -log p (|logits| + |lse|, plus the logits' own error
+    scale carried through log_softmax), d CE / d logits (p sum S + S, plus
+    p's error scale) pushed through the parental-logits VJP with |F| (the
+    parent distributions are >= 0, so that VJP of magnitudes sums the terms'
+    magnitudes) -- times rtol, through update_seq's softmax VJP."""
+    from oracle import nk_ref as nk
+
+    _, parts = nk.landscape_loss(ancestors, masked_sequences, n_leaves, interactions, fitness,
+                                 adj, lambda_val, real_k, temperature, seq_mask)
+    S = parts["S"]
+    A = np.asarray(adj, dtype=np.float64)
+    n_all, L, Q = S.shape
+    X = S.reshape(n_all, -1)
+    rc = A.sum(1) + A.sum(0)
+    mag = (np.abs(rc)[:, None] * np.abs(X) + np.abs(A + A.T) @ np.abs(X)).reshape(S.shape)
+    if lambda_val > 0.0 and real_k > 0:
+        mask = np.ones(L) if seq_mask is None else np.asarray(seq_mask, dtype=np.float64)
+        parent = np.argmax(A, axis=1)
+        n_nonroot = float((np.arange(n_all) != parent).sum())
+        w = mask[None, :, None] * (lambda_val / (n_nonroot * float(mask.sum())))
+        logits = parts["logits"]
+        Fa = np.abs(np.asarray(fitness, dtype=np.float64))
+        Lmag = nk.compute_parental_logits(S[parent], interactions, Fa, real_k)
+        m = logits.max(-1, keepdims=True)
+        lse = m + np.log(np.exp(logits - m).sum(-1, keepdims=True))
+        p = np.exp(logits - lse)
+        Lp = Lmag + (p * Lmag).sum(-1, keepdims=True)  # log_softmax of the logits' error
+        mag = mag + (np.abs(logits) + np.abs(lse) + Lp) * w
+        sumS = S.sum(-1, keepdims=True)
+        dlog_mag = (p * sumS + S + p * Lp * sumS) * w
+        np.add.at(mag, parent, nk.parental_logits_vjp(S[parent], interactions, Fa, dlog_mag))
+    pa = S[n_leaves:]
+    return rtol * temperature * softmax_vjp_bound(pa, mag[n_leaves:])
+
+
 __all__ = ["simulate_leaves", "hamming", "int_cost", "random_leaves", "balanced_children",
            "weird_children", "random_topologies", "create_balanced_binary_tree",
-           "assert_grad_close", "cond_rtol", "assert_bound_close", "path_dmax", "marginal_rtol",
-           "assert_marginals_close", "clear_argmax_mask", "surrogate_grad_bounds"]
+           "assert_grad_close", "cond_rtol", "assert_bound_close", "assert_dp_close", "path_dmax", "marginal_rtol",
+           "assert_marginals_close", "clear_argmax_mask", "surrogate_grad_bounds", "softmax_vjp_bound",
+           "tree_param_select", "loss_grad_bounds", "landscape_grad_bound"]

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_grad_close, assert_marginals_close, hamming, int_cost, random_leaves,
+from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, hamming, int_cost, random_leaves,
                     random_topologies)
 from oracle.sankoff_ref import run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref
@@ -97,6 +97,7 @@ def test_softmin_fwd_grad_bigq_vs_fp64(device, tau, Q):
     f = eng.forward(lv, c, tau, dp=True, site_score=True)
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=1e-5)
     np.testing.assert_allclose(f.site_score.cpu().numpy(), ref["site_score"], rtol=1e-5)
+    assert_dp_close(_sm(f.dp), ref, 1e-5)
     dc, mg, _ = eng.backward(lv, c, tau, f.dp, marginals=True)
     rel = assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=1e-5)
     assert rel <= 1e-5

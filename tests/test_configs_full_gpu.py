@@ -31,7 +31,7 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_bound_close, assert_grad_close, hamming, random_leaves,
+from _cases import (assert_bound_close, assert_dp_close, assert_grad_close, hamming, random_leaves,
                     random_topologies, simulate_leaves, surrogate_grad_bounds)
 from oracle import cpu_port
 from oracle import tree_ref as T
@@ -105,6 +105,8 @@ def test_c4_full_batch_vs_cpu_port(device, B):
     sample = [0, B // 2 + 1, B - 1]
     ref = batched_fwd_bwd_ref(ch[sample], leaves[sample], cost, tau)
     np.testing.assert_allclose(ts[sample], ref["tree_score"], rtol=SOFT_RTOL)
+    # the sampled trees' DP tables (what the fused kernel writes), per entry
+    assert_dp_close(f.dp[sample].transpose(2, 3).cpu().numpy(), ref, SOFT_RTOL)
     dts = torch.zeros(B, device=device)
     dts[sample] = 1.0
     ds, _, _ = eng.backward(lv, c, tau, f.dp, dts)

@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import assert_grad_close, int_cost, random_leaves
+from _cases import assert_bound_close, assert_grad_close, int_cost, random_leaves
 from oracle.sankoff_ref import run_sankoff_ref
 from oracle.softmin_ref import sankoff_fwd_bwd_ref
 from trex_amd import SankoffEngine, TreePlan, random_topologies
@@ -91,6 +91,10 @@ def test_ragged_softmin_fused_vs_oracle(device, tau, Q):
     np.testing.assert_allclose(ts.cpu().numpy(), [r["tree_score"] for r in refs], rtol=1e-5)
     ref_dc = sum(r["d_cost"] for r in refs)
     assert_grad_close(dc.cpu().numpy(), ref_dc, rtol=1e-5)
+    dpn = dp.cpu().numpy()
+    for b, r in enumerate(refs):  # per-entry DP bar (tests/_cases.py assert_dp_close)
+        assert_bound_close(plan.tree_rows(dpn, b).transpose(0, 2, 1), r["dp"],
+                           1e-5 * r["dp_mag"] + 1e-30, what=f"dp[{b}]")
     # fused == separate launches, bitwise
     ts2, dp2, _ = eng.forward(lv, c, tau)
     dc2, mg2, _ = eng.backward(lv, c, tau, dp2, torch.as_tensor(dts, dtype=torch.float32),

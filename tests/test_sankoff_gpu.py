@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_grad_close, assert_marginals_close, balanced_children,
+from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, balanced_children,
                     clear_argmax_mask, cond_rtol, hamming, int_cost, random_leaves,
                     random_topologies, simulate_leaves, weird_children)
 from oracle.sankoff_ref import normalize_leaves, run_sankoff_ref
@@ -225,6 +225,7 @@ def test_softmin_fwd_grad_vs_fp64(device, tau, L, n):
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     np.testing.assert_allclose(f.site_score.cpu().numpy(), ref["site_score"], rtol=SOFT_RTOL,
                                atol=1e-5)
+    assert_dp_close(_rows(eng, f.dp), ref, SOFT_RTOL)
     dc, mg, anc = eng.backward(lv, c, tau, f.dp, marginals=True, anc_states=True)
     assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
     # per-site marginals are products of softmax weights of D / tau along the
@@ -329,6 +330,7 @@ def test_c4_scale_properties(device):
     ref = batched_fwd_bwd_ref(ch[sample], leaves[sample], cost, tau)
     np.testing.assert_allclose(f1.tree_score.cpu().numpy()[sample], ref["tree_score"],
                                rtol=SOFT_RTOL)
+    assert_dp_close(_rows(eng, f1.dp)[sample], ref, SOFT_RTOL)
     dts = torch.zeros(B, device=device)
     dts[sample] = 1.0
     ds, _, _ = eng.backward(lv, c, tau, f1.dp, dts)
@@ -436,3 +438,4 @@ def test_config_c2_full_size_softmin_fwd_grad(device, tau, sim):
     fwd, dc, _, _ = eng.fwd_bwd(_dev(leaves, device), _dev(cost, device, torch.float32), tau)
     np.testing.assert_allclose(fwd.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
+    assert_dp_close(_rows(eng, fwd.dp), ref, SOFT_RTOL)

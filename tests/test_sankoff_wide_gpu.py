@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_grad_close, assert_marginals_close, clear_argmax_mask, cond_rtol,
+from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, clear_argmax_mask, cond_rtol,
                     hamming, int_cost, random_leaves, random_topologies)
 from oracle.sankoff_ref import run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref
@@ -143,6 +143,7 @@ def test_softmin_fwd_grad_wide_vs_fp64(device, tau, L, n, Q):
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     np.testing.assert_allclose(f.site_score.cpu().numpy(), ref["site_score"], rtol=SOFT_RTOL,
                                atol=1e-5)
+    assert_dp_close(_sm(f.dp), ref, SOFT_RTOL)
     dc, mg, anc = eng.backward(lv, c, tau, f.dp, marginals=True, anc_states=True)
     assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
     m = ref["marginals"]
@@ -247,12 +248,11 @@ def test_c3_scale_properties(device):
     ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
     np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
     assert_grad_close(dc.cpu().numpy(), ref["d_cost"], rtol=SOFT_RTOL)
-    # full-size DP table (D sums messages of either sign, so entries near 0
-    # carry the absolute error of their terms: rtol 1e-5 with 1e-5 max|D|),
-    # marginals and soft ancestral states (the elementwise marginal rule of
+    # full-size DP table, per entry at 1e-5 of its terms' magnitudes (D sums
+    # messages of either sign: tests/_cases.py assert_dp_close), marginals and
+    # soft ancestral states (the elementwise marginal rule of
     # tests/test_sankoff_gpu.py: fp32 D's conditioning along the root path)
-    np.testing.assert_allclose(_sm(f.dp), ref["dp"], rtol=SOFT_RTOL,
-                               atol=SOFT_RTOL * np.abs(ref["dp"]).max())
+    assert_dp_close(_sm(f.dp), ref, SOFT_RTOL)
     m = ref["marginals"]
     _, rt = assert_marginals_close(_sm(mg), m, ch, ref["dp"], tau)
     clear = clear_argmax_mask(m, rt)

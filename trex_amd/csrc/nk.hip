@@ -475,6 +475,280 @@ __global__ __launch_bounds__(kNkPP) void nk_logits_bwd_pp_kernel(NkArgs a,
   for (int b = t; b < nbin; b += kNkPP) G[((size_t)r * a.L + site) * nbin + b] = redb[b * kNkPP];
 }
 
+// ---- register kernels for small joint spaces (Q = 4, k <= 4; Q = 2,
+// k <= 6; the DNA shape, 255 parents x 2 000 sites, Q 4, k 4) ------------------
+// The wave-per-64-parents kernels above take each lane's prefix factors from
+// its LDS block and wait on a scalar load chain per F value (≈10 % of the
+// VALU peak).  Here Q and k are compile-time and a lane holds PPL parents'
+// k neighbour distributions in VGPRs.  The digits of neighbours 0..k-3 run
+// as nested rolled loops (each rotates its neighbour's Q factors -- and in
+// the reverse its Q bins -- by one register after every iteration, so the
+// current digit's value always sits in slot 0: no indexed register access)
+// around an unrolled body over neighbour k-2's digit and the last
+// neighbour's state; each body issues its 4 Q^2 F values as wide scalar
+// loads, and every F value feeds PPL parents.  The arithmetic per (parent,
+// site) is the rolled kernel's at NS = 1 step for step (the same products,
+// fmas and their order): the results are bitwise equal to it.
+constexpr int nk_cpow(int b, int e) { return e <= 0 ? 1 : b * nk_cpow(b, e - 1); }
+
+constexpr int kNkRegSites = 4;  // sites (waves) per block
+
+template <int Q>
+__device__ __forceinline__ void nk_rot(float (&v)[Q]) {
+  const float t = v[0];
+#pragma unroll
+  for (int c = 0; c < Q - 1; ++c) v[c] = v[c + 1];
+  v[Q - 1] = t;
+}
+
+template <int Q, int K, int PPL>
+__device__ __forceinline__ void nk_reg_gather(const NkArgs& a, int site, int lane,
+                                              float (&f)[PPL][K][Q], int (&rr)[PPL]) {
+  const cptr<int32_t> inter = as_const(a.inter) + (size_t)site * K;
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+    const int r = (blockIdx.x * PPL + p) * kWave + lane;
+    rr[p] = r < a.R ? r : -1;
+    const int row = r < a.R ? a.rows[r] : 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const float* src = a.S + ((size_t)row * a.L + inter[j]) * Q;
+      if constexpr (Q == 4) {
+        const float4 v = r < a.R ? *reinterpret_cast<const float4*>(src) : make_float4(0, 0, 0, 0);
+        f[p][j][0] = v.x;
+        f[p][j][1] = v.y;
+        f[p][j][2] = v.z;
+        f[p][j][3] = v.w;
+      } else {
+        const float2 v = r < a.R ? *reinterpret_cast<const float2*>(src) : make_float2(0, 0);
+        f[p][j][0] = v.x;
+        f[p][j][1] = v.y;
+      }
+    }
+  }
+}
+
+// forward body: the Q outer states of one setting of the rolled digits
+// (their factors in slot 0 of f[p][0..k-3]); F at this body's first entry
+template <int Q, int K, int PPL>
+__device__ __forceinline__ void nk_fwd_body(const float (&f)[PPL][K][Q], cptr<float> F,
+                                            float (&acc)[PPL][Q]) {
+  constexpr int QK = nk_cpow(Q, K);
+  constexpr int NI = K >= 2 ? Q : 1;
+  float ph[PPL];  // ((f_0 f_1) ...) f_{k-3}
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+    ph[p] = 1.0f;
+#pragma unroll
+    for (int j = 0; j < K - 2; ++j) ph[p] = j == 0 ? f[p][j][0] : ph[p] * f[p][j][0];
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+#pragma unroll
+    for (int c = 0; c < Q; ++c) {
+#pragma unroll
+      for (int p = 0; p < PPL; ++p) {
+        float pv;
+        if constexpr (K == 1)
+          pv = f[p][0][c];
+        else if constexpr (K == 2)
+          pv = f[p][0][i] * f[p][1][c];
+        else
+          pv = (ph[p] * f[p][K - 2][i]) * f[p][K - 1][c];
+#pragma unroll
+        for (int s = 0; s < Q; ++s) acc[p][s] = fmaf(F[s * QK + i * Q + c], pv, acc[p][s]);
+      }
+    }
+  }
+}
+
+// rolled digit J (J < k - 2): Q iterations, neighbour J's factors rotated
+template <int Q, int K, int PPL, int J>
+__device__ __forceinline__ void nk_fwd_loop(float (&f)[PPL][K][Q], cptr<float> F,
+                                            float (&acc)[PPL][Q]) {
+  if constexpr (J >= K - 2) {
+    nk_fwd_body<Q, K, PPL>(f, F, acc);
+  } else {
+    constexpr int step = nk_cpow(Q, K - 1 - J) * Q;  // F entries per digit-J value
+#pragma unroll 1
+    for (int d = 0; d < Q; ++d) {
+      nk_fwd_loop<Q, K, PPL, J + 1>(f, F + d * step, acc);
+#pragma unroll
+      for (int p = 0; p < PPL; ++p) nk_rot<Q>(f[p][J]);
+    }
+  }
+}
+
+template <int Q, int K, int PPL>
+__global__ __launch_bounds__(kWave * kNkRegSites) __attribute__((amdgpu_waves_per_eu(4))) void nk_logits_reg_kernel(NkArgs a,
+                                                                            float* __restrict__ logits) {
+  constexpr int QK = nk_cpow(Q, K);
+  const int site = __builtin_amdgcn_readfirstlane(blockIdx.y * kNkRegSites + threadIdx.y);
+  if (site >= a.L) return;
+  const int lane = threadIdx.x;
+  float f[PPL][K][Q];
+  int rr[PPL];
+  nk_reg_gather<Q, K, PPL>(a, site, lane, f, rr);
+  float acc[PPL][Q];
+#pragma unroll
+  for (int p = 0; p < PPL; ++p)
+#pragma unroll
+    for (int s = 0; s < Q; ++s) acc[p][s] = 0.0f;
+  nk_fwd_loop<Q, K, PPL, 0>(f, as_const(a.F) + (size_t)site * QK * Q, acc);
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+    if (rr[p] < 0) continue;
+    float* o = logits + ((size_t)rr[p] * a.L + site) * Q;
+    if constexpr (Q == 4)
+      *reinterpret_cast<float4*>(o) = make_float4(acc[p][0], acc[p][1], acc[p][2], acc[p][3]);
+    else
+      *reinterpret_cast<float2*>(o) = make_float2(acc[p][0], acc[p][1]);
+  }
+}
+
+// reverse body: the rolled nk_logits_bwd_kernel's per-outer-state steps
+// (prefix x suffix products E_j, dJ_c, the last neighbour's bins, T, the
+// other neighbours' bins) for the Q outer states of one rolled setting;
+// neighbour j < k-2's current factor and bin sit in slot 0
+template <int Q, int K, int PPL>
+__device__ __forceinline__ void nk_bwd_body(const float (&f)[PPL][K][Q], const float (&gs)[PPL][Q],
+                                            cptr<float> F, float (&gb)[PPL][K][Q]) {
+  constexpr int QK = nk_cpow(Q, K);
+  constexpr int NI = K >= 2 ? Q : 1;
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      float fv[K], E[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        fv[j] = j < K - 2 ? f[p][j][0] : (j == K - 2 ? f[p][j][i] : 1.0f);
+      float pre = 1.0f;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        E[j] = pre;
+        pre *= fv[j];
+      }
+      float suf = 1.0f;
+#pragma unroll
+      for (int j = K - 1; j >= 0; --j) {
+        E[j] *= suf;
+        suf *= fv[j];
+      }
+      float T = 0.0f;
+#pragma unroll
+      for (int c = 0; c < Q; ++c) {
+        float dj = 0.0f;
+#pragma unroll
+        for (int s = 0; s < Q; ++s) dj = fmaf(gs[p][s], F[s * QK + i * Q + c], dj);
+        gb[p][K - 1][c] = fmaf(dj, pre, gb[p][K - 1][c]);
+        T = fmaf(dj, f[p][K - 1][c], T);
+      }
+#pragma unroll
+      for (int j = 0; j < K - 1; ++j) {
+        const int d = j < K - 2 ? 0 : i;
+        gb[p][j][d] = fmaf(E[j], T, gb[p][j][d]);
+      }
+    }
+  }
+}
+
+template <int Q, int K, int PPL, int J>
+__device__ __forceinline__ void nk_bwd_loop(float (&f)[PPL][K][Q], const float (&gs)[PPL][Q],
+                                            cptr<float> F, float (&gb)[PPL][K][Q]) {
+  if constexpr (J >= K - 2) {
+    nk_bwd_body<Q, K, PPL>(f, gs, F, gb);
+  } else {
+    constexpr int step = nk_cpow(Q, K - 1 - J) * Q;
+#pragma unroll 1
+    for (int d = 0; d < Q; ++d) {
+      nk_bwd_loop<Q, K, PPL, J + 1>(f, gs, F + d * step, gb);
+#pragma unroll
+      for (int p = 0; p < PPL; ++p) {
+        nk_rot<Q>(f[p][J]);
+        nk_rot<Q>(gb[p][J]);
+      }
+    }
+  }
+}
+
+template <int Q, int K, int PPL>
+__global__ __launch_bounds__(kWave * kNkRegSites) void nk_logits_bwd_reg_kernel(
+    NkArgs a, const float* __restrict__ g, float* __restrict__ G) {
+  constexpr int QK = nk_cpow(Q, K);
+  const int site = __builtin_amdgcn_readfirstlane(blockIdx.y * kNkRegSites + threadIdx.y);
+  if (site >= a.L) return;
+  const int lane = threadIdx.x;
+  float f[PPL][K][Q];
+  int rr[PPL];
+  nk_reg_gather<Q, K, PPL>(a, site, lane, f, rr);
+  float gs[PPL][Q], gb[PPL][K][Q];
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+    const float* gp = g + ((size_t)(rr[p] < 0 ? 0 : rr[p]) * a.L + site) * Q;
+#pragma unroll
+    for (int s = 0; s < Q; ++s) gs[p][s] = rr[p] < 0 ? 0.0f : gp[s];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int c = 0; c < Q; ++c) gb[p][j][c] = 0.0f;
+  }
+  nk_bwd_loop<Q, K, PPL, 0>(f, gs, as_const(a.F) + (size_t)site * QK * Q, gb);
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+    if (rr[p] < 0) continue;
+    float* o = G + (((size_t)rr[p] * a.L + site) * K) * Q;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if constexpr (Q == 4)
+        *reinterpret_cast<float4*>(o + j * Q) = make_float4(gb[p][j][0], gb[p][j][1], gb[p][j][2], gb[p][j][3]);
+      else
+        *reinterpret_cast<float2*>(o + j * Q) = make_float2(gb[p][j][0], gb[p][j][1]);
+    }
+  }
+}
+
+// the register kernels take (Q, k) with Q^(k-1) <= 64 at Q = 4 or 2
+bool nk_use_reg(int Q, int k) {
+  const char* e = std::getenv("TREX_NK_REG");  // A/B: "0" keeps the rolled kernels (read per call)
+  if (e && e[0] == '0') return false;
+  return (Q == 4 && k >= 1 && k <= 4) || (Q == 2 && k >= 1 && k <= 6);
+}
+
+constexpr int kNkRegPplFwd = 2, kNkRegPplBwd = 2;
+
+template <int Q, int K>
+void nk_reg_launch(const NkArgs& a, hipStream_t st, float* logits, const float* g, float* G) {
+  const int ppl = logits ? kNkRegPplFwd : kNkRegPplBwd;
+  const dim3 grid((a.R + kWave * ppl - 1) / (kWave * ppl), (a.L + kNkRegSites - 1) / kNkRegSites);
+  const dim3 block(kWave, kNkRegSites);
+  if (logits)
+    hipLaunchKernelGGL((nk_logits_reg_kernel<Q, K, kNkRegPplFwd>), grid, block, 0, st, a, logits);
+  else
+    hipLaunchKernelGGL((nk_logits_bwd_reg_kernel<Q, K, kNkRegPplBwd>), grid, block, 0, st, a, g, G);
+}
+
+// logits (g, G null) or their reverse (logits null)
+void nk_reg_run(const NkArgs& a, hipStream_t st, float* logits, const float* g, float* G) {
+  if (a.Q == 4) {
+    switch (a.k) {
+      case 1: nk_reg_launch<4, 1>(a, st, logits, g, G); break;
+      case 2: nk_reg_launch<4, 2>(a, st, logits, g, G); break;
+      case 3: nk_reg_launch<4, 3>(a, st, logits, g, G); break;
+      default: nk_reg_launch<4, 4>(a, st, logits, g, G); break;
+    }
+  } else {
+    switch (a.k) {
+      case 1: nk_reg_launch<2, 1>(a, st, logits, g, G); break;
+      case 2: nk_reg_launch<2, 2>(a, st, logits, g, G); break;
+      case 3: nk_reg_launch<2, 3>(a, st, logits, g, G); break;
+      case 4: nk_reg_launch<2, 4>(a, st, logits, g, G); break;
+      case 5: nk_reg_launch<2, 5>(a, st, logits, g, G); break;
+      default: nk_reg_launch<2, 6>(a, st, logits, g, G); break;
+    }
+  }
+}
+
 // the per-pair kernels for few (parent, site) pairs with many joint states
 bool nk_use_pp(int R, int L, int Q, int k, int QK) {
   if (k == 0 || (Q != 2 && Q != 4)) return false;
@@ -632,6 +906,10 @@ bool launch_logits(const NkArgs& a, int ns, hipStream_t st, float* logits,
     }
     return ce != nullptr;
   }
+  if (nk_use_reg(a.Q, a.k)) {
+    nk_reg_run(a, st, logits, nullptr, nullptr);
+    return false;
+  }
   const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);
   const size_t lds = nk_fwd_lds(a.Q, a.k, ns);
   switch (a.Q) {
@@ -651,6 +929,10 @@ void launch_logits_bwd(const NkArgs& a, int ns, hipStream_t st, const float* g, 
       hipLaunchKernelGGL(nk_logits_bwd_pp_kernel<2>, grid, dim3(kNkPP), lds, st, a, g, G);
     else
       hipLaunchKernelGGL(nk_logits_bwd_pp_kernel<4>, grid, dim3(kNkPP), lds, st, a, g, G);
+    return;
+  }
+  if (nk_use_reg(a.Q, a.k)) {
+    nk_reg_run(a, st, nullptr, g, G);
     return;
   }
   const dim3 grid((a.R + kWave - 1) / kWave, a.L), block(kWave, ns);
