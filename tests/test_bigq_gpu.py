@@ -15,8 +15,8 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, hamming, int_cost, random_leaves,
-                    random_topologies)
+from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, hamming,
+                    int_cost, random_leaves, random_topologies)
 from oracle.sankoff_ref import run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref
 from trex_amd import SankoffEngine, TreePlan, TrexError, run_sankoff

@@ -17,8 +17,8 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, balanced_children,
-                    clear_argmax_mask, cond_rtol, hamming, int_cost, random_leaves,
+from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close,
+                    balanced_children, clear_argmax_mask, cond_rtol, hamming, int_cost, random_leaves,
                     random_topologies, simulate_leaves, weird_children)
 from oracle.sankoff_ref import normalize_leaves, run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref

@@ -17,8 +17,9 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, clear_argmax_mask, cond_rtol,
-                    hamming, int_cost, random_leaves, random_topologies)
+from _cases import (assert_dp_close, assert_grad_close, assert_marginals_close, balanced_children,
+                    clear_argmax_mask, cond_rtol, hamming, int_cost, random_leaves,
+                    random_topologies)
 from oracle.sankoff_ref import run_sankoff_ref
 from oracle.softmin_ref import batched_fwd_bwd_ref
 from trex_amd import SankoffEngine, TreePlan, run_sankoff
@@ -305,3 +306,37 @@ def test_site_gate_repeat_calls_no_sync(device, tau, wide_kernel):
         f, dc, mg, _ = eng.fwd_bwd(lv, c, tau, marginals=True)
         assert torch.equal(f.tree_score, ref2[0]) and torch.equal(dc, ref2[1]), i
         assert torch.equal(mg, ref2[2]), i
+
+
+@pytest.mark.parametrize("topo", ["balanced", "random"])
+@pytest.mark.parametrize("Q", [20, 13])
+def test_site_cherry_tables_are_bitwise_neutral(device, monkeypatch, topo, Q):
+    """The lane-per-site kernel's cherry tables (wide_dev.h site_pair_tables:
+    a height-1 row's forward message and softmin row sums by its children's
+    code pair, built by the gate) == the per-lane mat-vecs they replace
+    (TREX_SITE_CHERRY=0), bit for bit: DP table, scores, dC, marginals and
+    soft ancestral states, fused and separate launches, with missing leaf
+    states (code Q: the all-1e5 row's message) and cherries both under
+    height-2 rows and directly under task rows (random topologies)."""
+    B, n, L, tau = 2, 64, 777, 0.5
+    ch = (balanced_children(n, B) if topo == "balanced" else random_topologies(B, n, seed=71))
+    leaves = random_leaves(B, n, L, Q, seed=72, missing=0.03)
+    cost = int_cost(Q, seed=73)
+    lv, c = _dev(leaves, device), _dev(cost, device, torch.float32)
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TREX_SITE_CHERRY", flag)
+        eng = _engine(ch, L, Q, device)
+        f, dc, mg, an = eng.fwd_bwd(lv, c, tau, site_score=True, marginals=True,
+                                    anc_states=True)
+        f2 = eng.forward(lv, c, tau)
+        dc2, _, _ = eng.backward(lv, c, tau, f2.dp)
+        torch.cuda.synchronize()
+        runs.append((f.dp.clone(), f.tree_score.clone(), f.site_score.clone(), dc.clone(),
+                     mg.clone(), an.clone(), f2.dp.clone(), dc2.clone()))
+    for a, b, what in zip(runs[0], runs[1], ("dp", "tree", "site", "dC", "marg", "anc", "dp2",
+                                             "dC2")):
+        assert torch.equal(a, b), what
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
+    assert_grad_close(runs[0][3].cpu().numpy(), ref["d_cost"], rtol=cond_rtol(ref["dp"], tau))
+    assert_dp_close(_sm(runs[0][0]), ref, SOFT_RTOL)

@@ -70,6 +70,8 @@ struct SiteArgs {
   double* part_tree;  // [B * tiles]
   double* part_dc;    // [Q * Q][B * tiles]
   const float* kg;    // K [kSQ][kSQ] and K^T (site_gate_write), zero-padded
+  const float* ptab;  // cherry tables TM | TS (site_pair_tables), below K
+  int cherry;         // 0: no tables (TREX_SITE_CHERRY=0, A/B; bitwise the same)
   const int* flag;    // 1: this kernel handles the launch
   int n_slots;
 };
@@ -263,11 +265,27 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
   auto leaf_code = [&](int desc) -> int {
     return ((desc >> 24) & 3) == kKindLeaf ? (int)lleaf[(desc & 0xFFFF) * kWave + lane] : Q;
   };
+  // cherry tables (wide_dev.h site_pair_tables): a height-1 row's forward
+  // message (TM) and softmin row sums (TS) by its children's code pair
+  const float* tmg = A.ptab;
+  const float* tsg = A.ptab + kSitePairs * kSQ;
+  auto pair_of = [&](const I4& e) -> int { return site_pair(leaf_code(e.y), leaf_code(e.z)); };
+  auto load_tab = [&](const float* t, int p, float (&v)[kSQ]) {
+    const float4* r = reinterpret_cast<const float4*>(t + p * kSQ);
+#pragma unroll
+    for (int c = 0; c < kSQ / 4; ++c) {
+      const float4 w = r[c];
+      v[4 * c] = w.x;
+      v[4 * c + 1] = w.y;
+      v[4 * c + 2] = w.z;
+      v[4 * c + 3] = w.w;
+    }
+  };
 
   // softmin weights of a child with D = d: md = min_j D_j, u_j = exp2((md - D_j) a),
   // s_i = sum_j K_ij u_j (K rows by scalar loads, two partial sums in packed
   // FP32; s_i staged through the wave's scratch, row i at i * 64 + lane)
-  auto weights = [&](const float (&d)[kSQ], float& md, float (&u)[kSQ], float (&s)[kSQ]) {
+  auto weights_u = [&](const float (&d)[kSQ], float& md, float (&u)[kSQ]) {
     float m0 = d[0];
 #pragma unroll
     for (int j = 1; j < kSQ; ++j) m0 = j < Q ? fminf(m0, d[j]) : m0;
@@ -275,6 +293,9 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     const float mda = md * a;
 #pragma unroll
     for (int j = 0; j < kSQ; ++j) u[j] = j < Q ? fast_exp2(fmaf(-d[j], a, mda)) : 0.0f;
+  };
+  auto weights = [&](const float (&d)[kSQ], float& md, float (&u)[kSQ], float (&s)[kSQ]) {
+    weights_u(d, md, u);
     // s += K[:, j] u_j over j: independent accumulators (a row-wise dot
     // product would be a chain of dependent FMAs); u_j staged through the
     // scratch, column j of K (= row j of K^T) by scalar loads
@@ -325,6 +346,19 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     leaf_add(e.y, d, true);
     leaf_add(e.z, d, false);
   };
+  // a cherry's (height-1 row's) message from TM, its D row stored when
+  // `store` -- bitwise cheap_d + message_add
+  auto cherry_add = [&](const I4& e, float (&dv)[kSQ], bool first, bool store) {
+    float m[kSQ];
+    load_tab(tmg, pair_of(e), m);
+    if (store) {
+      float d[kSQ];
+      cheap_d(e, d);
+      store_row(rdp, e.x, d);
+    }
+#pragma unroll
+    for (int i = 0; i < kSQ; ++i) dv[i] = first ? m[i] : dv[i] + m[i];
+  };
   // D of an inline row (height 1 or 2); `store`: write its DP row
   auto inline_d = [&](int idx, float (&d)[kSQ], bool store) {
     const I4 e = load_step(inl, idx);
@@ -336,10 +370,14 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         const int desc = c == 0 ? e.y : e.z;
         if (((desc >> 24) & 3) == kKindInline) {
           const I4 e2 = load_step(inl, desc & 0xFFFF);
-          float dc[kSQ];
-          cheap_d(e2, dc);
-          if (store) store_row(rdp, e2.x, dc);
-          message_add(dc, d, c == 0);
+          if (A.cherry) {
+            cherry_add(e2, d, c == 0, store);
+          } else {
+            float dc[kSQ];
+            cheap_d(e2, dc);
+            if (store) store_row(rdp, e2.x, dc);
+            message_add(dc, d, c == 0);
+          }
         } else {
           leaf_add(desc, d, c == 0);
         }
@@ -355,9 +393,14 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
       slot_get((desc >> 16) & 0xFF, d);
       message_add(d, dv, first);
     } else if (kind == kKindInline) {
-      float d[kSQ];
-      inline_d(desc & 0xFFFF, d, store);
-      message_add(d, dv, first);
+      const I4 e = load_step(inl, desc & 0xFFFF);
+      if (e.w <= 1 && A.cherry) {
+        cherry_add(e, dv, first, store);
+      } else {
+        float d[kSQ];
+        inline_d(desc & 0xFFFF, d, store);
+        message_add(d, dv, first);
+      }
     } else {
       leaf_add(desc, dv, first);
     }
@@ -560,9 +603,8 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     };
     // adjoint of one internal child with D = d under parent cotangent g:
     // w_ij = K_ij u_j / s_i, r_i = g_i / s_i; dC += r u^T (x K); gc_j = u_j sum_i K_ij r_i
-    auto child_adj = [&](const float (&d)[kSQ], const float (&g)[kSQ], float (&gc)[kSQ]) {
-      float md, u[kSQ], r[kSQ];
-      weights(d, md, u, r);
+    auto child_adj_rest = [&](const float (&u)[kSQ], float (&r)[kSQ], const float (&g)[kSQ],
+                              float (&gc)[kSQ]) {
 #pragma unroll
       for (int i = 0; i < kSQ; ++i) r[i] = i < Q ? g[i] * __builtin_amdgcn_rcpf(r[i]) : 0.0f;
 #pragma unroll
@@ -593,6 +635,23 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         gc[j + 1] = u[j + 1] * t2[j / 2].y;
       }
       outer_mfma();
+    };
+    auto child_adj = [&](const float (&d)[kSQ], const float (&g)[kSQ], float (&gc)[kSQ]) {
+      float md, u[kSQ], r[kSQ];
+      weights(d, md, u, r);
+      child_adj_rest(u, r, g, gc);
+    };
+    // a cherry child: its row sums s from TS (the forward's mat-vec, bitwise)
+    auto cherry_adj = [&](const I4& e, const float (&d)[kSQ], const float (&g)[kSQ],
+                          float (&gc)[kSQ]) {
+      if (!A.cherry) {
+        child_adj(d, g, gc);
+        return;
+      }
+      float md, u[kSQ], r[kSQ];
+      load_tab(tsg, pair_of(e), r);
+      weights_u(d, md, u);
+      child_adj_rest(u, r, g, gc);
     };
     // a 1e5-row child: u = 1 on every state, r_i = g_i / sum_j K_ij
     auto sent_adj = [&](const float (&g)[kSQ]) {
@@ -659,7 +718,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
             const I4 e2 = load_step(inl, desc & 0xFFFF);
             float dc[kSQ], gc[kSQ];
             cheap_d(e2, dc);
-            child_adj(dc, g, gc);
+            cherry_adj(e2, dc, g, gc);
             emit(e2.x, gc);
             leafish_adj(gc, e2.y, e2.z);
           }
@@ -691,7 +750,10 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
               cheap_d(ie, d);
             slot_get(vslot, g);
             if (c == 0) emit(stp.x & 0xFFFF, g);
-            child_adj(d, g, gc);
+            if (ie.w > 1)
+              child_adj(d, g, gc);
+            else
+              cherry_adj(ie, d, g, gc);
             if (kind == kKindInt)
               slot_put((desc >> 16) & 0xFF, gc);
             else
@@ -803,6 +865,11 @@ int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slo
   A.part_tree = static_cast<double*>(c.workspace);
   A.part_dc = A.part_tree + nb;
   A.kg = kg;
+  A.ptab = kg - kSiteTabBytes / 4;
+  {
+    const char* e = std::getenv("TREX_SITE_CHERRY");  // read per call (tests flip it)
+    A.cherry = !(e && e[0] == '0');
+  }
   A.flag = flag;
   A.n_slots = lp_slots;
   auto go = [&](auto kernel) {

@@ -378,7 +378,12 @@ __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_
       const float gmin = uniform(wave_minf(lmin)), gmax = uniform(wave_maxf(lmax));
       const bool handled = site_takes_call(gmin, gmax, A.a);
       if (blockIdx.x == 0) site_gate_write(A.cost, Q, gmin, A.a, A.site_kg, A.site_flag, handled);
-      if (handled) return;
+      if (handled) {
+        // the first workgroups build the cherry tables below K
+        __shared__ float kl[kSiteSQ * kSiteSQ];
+        site_pair_tables(A.cost, Q, gmin, A.a, A.bcoef, A.site_kg - kSiteTabBytes / 4, kl);
+        return;
+      }
     }
   }
   float cmin, cmax;
@@ -758,9 +763,10 @@ size_t wide_lds_bytes(int n_slots, int nl, int ni, int Q) {
 
 int64_t wide_workspace_bytes(int B, int L, int Q) {
   const int64_t nb = (int64_t)B * wide_tiles(L, Q);
-  // tail: staged-kernel counter (128 B) | K and K^T for the lane-per-site
-  // kernel (3.25 KB, sankoff_site.hip) | mode flag (128 B)
-  return nb * 8 * (1 + (int64_t)Q * Q) + 3584;
+  // tail: staged-kernel counter (128 B) | cherry tables (36 KB) and K and
+  // K^T (3.25 KB) for the lane-per-site kernel (sankoff_site.hip) | mode
+  // flag (128 B)
+  return nb * 8 * (1 + (int64_t)Q * Q) + 3584 + kSiteTabBytes;
 }
 
 int wide_run(const char* fn, const WideCall& c, bool reduce) {

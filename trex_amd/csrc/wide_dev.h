@@ -155,6 +155,68 @@ __device__ __forceinline__ void site_gate_write(const float* cost, int Q, float 
   if (lane == 0) flag[0] = handled ? 1 : 0;
 }
 
+// ---- cherry tables of the lane-per-site kernel ----
+// A cherry (an internal row whose two children are leaves or 1e5 rows) has
+// D = T[c0] + T[c1], with T the leaf-message table (T[c][i] = C[i][c],
+// T[Q] the all-1e5 row's message): one of (Q + 1)(Q + 2) / 2 vectors.  The
+// gate builds, per unordered code pair, the cherry's forward message to its
+// parent (TM) and its softmin row sums s = K u (TS), with the site kernel's
+// arithmetic step for step (bitwise what it would compute per lane), so the
+// site kernel replaces a cherry's K mat-vec -- both of the forward's and one
+// of the adjoint's -- by a table row.  Workspace: TM [pairs][20] | TS
+// [pairs][20] just below K / K^T.
+constexpr int kSitePairs = (kSiteSQ + 1) * (kSiteSQ + 2) / 2;
+constexpr int kSiteTabBytes = (2 * kSitePairs * kSiteSQ * 4 + 127) / 128 * 128;
+__device__ __forceinline__ int site_pair(int c0, int c1) {
+  const int lo = c0 < c1 ? c0 : c1, hi = c0 < c1 ? c1 : c0;
+  return hi * (hi + 1) / 2 + lo;
+}
+// the workgroups of the gate share the pairs (64 per workgroup and round);
+// kl: [kSiteSQ * kSiteSQ] floats of LDS for this workgroup's copy of K
+__device__ __forceinline__ void site_pair_tables(const float* cost, int Q, float cmin, float a,
+                                                 float bcoef, float* tm, float* kl) {
+  const int lane = threadIdx.x & (kWave - 1);
+  if ((int)blockIdx.x * kWave >= kSitePairs) return;
+  for (int e = lane; e < kSiteSQ * kSiteSQ; e += kWave) {
+    const int i = e / kSiteSQ, j = e - i * kSiteSQ;
+    kl[e] = (i < Q && j < Q) ? fast_exp2((cmin - cost[i * Q + j]) * a) : 0.0f;
+  }
+  __syncthreads();
+  float* ts = tm + kSitePairs * kSiteSQ;
+  for (int p = (int)blockIdx.x * kWave + lane; p < kSitePairs; p += (int)gridDim.x * kWave) {
+    int hi = 0;
+    while ((hi + 1) * (hi + 2) / 2 <= p) ++hi;
+    const int lo = p - hi * (hi + 1) / 2;
+    if (hi > Q) continue;  // codes are 0..Q
+    // T[c][i] as the site kernel's prologue builds it (sankoff_site.hip)
+    auto trow = [&](int code, int i) -> float {
+      if (i >= Q) return 0.0f;
+      if (code < Q) return cost[i * Q + code];
+      float sk = 0.0f;
+      for (int j = 0; j < Q; ++j) sk += kl[i * kSiteSQ + j];
+      return fmaf(-bcoef, fast_log2(sk), kSentinel + cmin);
+    };
+    float d[kSiteSQ], u[kSiteSQ];
+#pragma unroll
+    for (int i = 0; i < kSiteSQ; ++i) d[i] = trow(lo, i) + trow(hi, i);
+    float md = d[0];
+#pragma unroll
+    for (int j = 1; j < kSiteSQ; ++j) md = j < Q ? fminf(md, d[j]) : md;
+    const float mda = md * a;
+#pragma unroll
+    for (int j = 0; j < kSiteSQ; ++j) u[j] = j < Q ? fast_exp2(fmaf(-d[j], a, mda)) : 0.0f;
+    const float base = md + cmin;
+#pragma unroll
+    for (int i = 0; i < kSiteSQ; ++i) {
+      float s = 0.0f;
+      for (int j = 0; j < Q; ++j) s = fmaf(kl[i * kSiteSQ + j], u[j], s);
+      s = i < Q ? s : 1.0f;
+      ts[p * kSiteSQ + i] = s;
+      tm[p * kSiteSQ + i] = i < Q ? fmaf(-bcoef, fast_log2(s), base) : 0.0f;
+    }
+  }
+}
+
 template <int G>
 __device__ __forceinline__ void xor_perm_coefs(WCoef<G>& cf, int i);
 
