@@ -192,11 +192,26 @@ def marginal_rtol(children, dp_ref, tau, rtol=1e-5, c=8.0):
     """Per-entry relative bound for softmin marginals vs the fp64 oracle,
     (B, n_int, 1, L): max(rtol, c * 2^-24 * path_dmax / tau) -- fp32 D's
     conditioning along the root path (see path_dmax), never below 1e-5.
-    c = 8: measured on MI355X over every kernel and the tests' shapes (Q 4 ..
-    61, tau 0.02 .. 1, 8 .. 64 taxa, C3 at full size), the worst entry sat at
-    5.0 x eps * path_dmax / tau (tools/parity_probe.py marg,
-    profiles/r04_parity_probe.log); entries whose bound is 1e-5 stayed below
-    3e-6."""
+
+    c from the adjoint's rounding steps.  A marginal is a product of softmin
+    weights along its root path; each weight is exp((md - D_j) / tau) / s
+    with |md|, |D_j| <= dmax (the row's max |D|), so its relative error is
+    the absolute error of (md - D_j) / tau.  Per level, in units of
+    2^-24 dmax / tau (half an ulp of dmax):
+      * D_j as the kernel holds it: two messages, each rounded once after
+        its own log / fma (1 + 1), and their sum rounded (1)          -> 3
+      * md = min_j D_j: the same value, the same 3                     -> 3
+      * the subtraction md - D_j, rounded                               -> 1
+      * the scale by a = log2(e) / tau (1) and exp2's result (1 ulp of a
+        value <= 1: below the unit of the others)                      -> 1
+    c = 3 + 3 + 1 + 1 = 8 per level, summed over the path (path_dmax sums
+    each level's dmax).  The normalisations 1/s (s a sum of <= Q terms in
+    [0, 1]) add ~Q 2^-24 relative per level, independent of |D| / tau: that
+    is what the rtol floor 1e-5 covers.  Measured on MI355X over every
+    kernel and the tests' shapes (Q 4 .. 61, tau 0.02 .. 1, 8 .. 64 taxa, C3
+    at full size): worst entry 5.0 (tools/parity_probe.py marg,
+    profiles/r04_parity_probe.log), entries with the 1e-5 floor below 3e-6
+    -- inside the derived bound."""
     return np.maximum(rtol, c * 2.0 ** -24 * path_dmax(children, dp_ref) / tau)[:, :, None, :]
 
 
