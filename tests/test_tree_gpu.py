@@ -826,3 +826,25 @@ def test_tree_optimizer_presplit_operands_are_bitwise_neutral(device, monkeypatc
     for i in (1, 2, 3):
         for k in a[i]:
             assert torch.equal(a[i][k], b[i][k]), (i, k)
+
+
+def test_update_tree_and_compute_loss_take_a_key(device):
+    """The reference's key arguments (update_tree tree.py:71, compute_loss
+    tree.py:337): a PRNGKey draws the Gumbel noise on the device; the same
+    key gives the same adjacency, compute_loss splits the key as the
+    reference does (the second half draws update_tree's noise)."""
+    params, _, seqs = _tree_case(16, 20, 4, 3)
+    p = {k: _t(v, device) for k, v in params.items()}
+    key = G.PRNGKey(42)
+    shape = (params["tree_params"].shape[0], params["tree_params"].shape[1])
+    a1 = G.update_tree(key, p)
+    a2 = G.update_tree(G.gumbel(key, shape, device), p)
+    a3 = G.update_tree(G.PRNGKey(42), p)
+    assert torch.equal(a1, a2) and torch.equal(a1, a3)
+    assert not torch.equal(a1, G.update_tree(G.PRNGKey(43), p))
+    noise = G.gumbel(G.split(key)[1], shape, device)
+    l_key = float(G.compute_loss(key, p, _t(seqs, device), None, 0.7, None))
+    l_noise = float(G.compute_loss(noise, p, _t(seqs, device), None, 0.7, None))
+    assert l_key == l_noise
+    rl, _ = T.compute_loss(_n(noise), params, seqs, 0.7, None)
+    np.testing.assert_allclose(l_key, rl, rtol=RTOL)

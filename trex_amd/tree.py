@@ -87,6 +87,61 @@ def gumbel_noise_step(seed: int, step: int, shape, device=None, out=None):
 
 
 # ---------------------------------------------------------------------------
+# PRNG keys (the reference's `key` arguments)
+# ---------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    z = x
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+class PRNGKey:
+    """Stand-in for a ``jax.random.PRNGKey`` where the reference takes a key
+    (update_tree tree.py:71, compute_loss tree.py:337): a 64-bit seed whose
+    Gumbel draw is ``trex_gumbel_noise`` (a pure function of seed, step and
+    index), and ``split`` derives children by splitmix64.  JAX's threefry
+    stream itself cannot be reproduced without JAX, so draws differ from
+    trex's for the same integer seed; the call shapes and the determinism
+    (same key -> same noise, split keys independent) are the reference's."""
+
+    __slots__ = ("seed",)
+
+    def __init__(self, seed: int):
+        self.seed = int(seed) & _M64
+
+    def __repr__(self):
+        return f"PRNGKey({self.seed:#x})"
+
+    def __eq__(self, other):
+        return isinstance(other, PRNGKey) and other.seed == self.seed
+
+    def __hash__(self):
+        return hash(("trex_amd.PRNGKey", self.seed))
+
+
+def split(key: PRNGKey, num: int = 2):
+    """``jax.random.split(key, num)``'s role: ``num`` child keys."""
+    return tuple(PRNGKey(_splitmix64(key.seed ^ _splitmix64(i + 1))) for i in range(int(num)))
+
+
+def gumbel(key: PRNGKey, shape, device=None):
+    """Standard Gumbel noise of ``shape`` drawn from ``key`` on the device."""
+    return gumbel_noise_step(key.seed, 1, shape, device)
+
+
+def _tree_noise(noise, shape, device):
+    """update_tree's noise argument: a PRNGKey draws, a tensor is the noise."""
+    if isinstance(noise, PRNGKey):
+        return gumbel(noise, shape, device)
+    return _dev(noise, device) if noise is not None else None
+
+
+# ---------------------------------------------------------------------------
 # topology / sequences
 # ---------------------------------------------------------------------------
 def discretize_tree_topology(adjacency, n_nodes: int):
@@ -100,13 +155,15 @@ def discretize_tree_topology(adjacency, n_nodes: int):
 
 
 def update_tree(noise, params, temperature: float = 1.0, gates=None):
-    """Relaxed topology: row softmax of the masked logits (tree.py:50-107)."""
+    """Relaxed topology: row softmax of the masked logits (tree.py:50-107).
+    ``noise``: the Gumbel noise (n_nodes - 1, n_anc), or a PRNGKey to draw it
+    from (the reference's ``key``), or None (no noise)."""
     torch = _torch()
     theta = _dev(params["tree_params"])
     n_m1, n_anc = theta.shape
     N = n_m1 + 1
     dev = theta.device
-    nz = _dev(noise, dev) if noise is not None else None
+    nz = _tree_noise(noise, (n_m1, n_anc), dev)
     gt = _dev(gates, dev) if gates is not None else None
     A = torch.empty((N, N), dtype=torch.float32, device=dev)
     check(lib().trex_tree_update_tree(ptr(theta), ptr(nz), ptr(gt), N, n_anc, float(temperature),
@@ -223,8 +280,12 @@ def loss_and_grad(noise, params, sequences, temperature: float, adjacency=None, 
     """compute_loss (tree.py:336-342) and d loss / d params.
 
     update_tree runs at temperature 1.0: compute_loss does not pass T to it
-    (tree.py:338).  Returns (loss, {"tree_params", "ancestors"}).
+    (tree.py:338).  ``noise``: update_tree's Gumbel noise, or a PRNGKey,
+    split as the reference splits its key (tree.py:337: the second half
+    draws the noise).  Returns (loss, {"tree_params", "ancestors"}).
     """
+    if isinstance(noise, PRNGKey):
+        noise = split(noise)[1]
     torch = _torch()
     theta = _dev(params["tree_params"])
     anc = _ancestors(params)
@@ -259,7 +320,8 @@ def loss_and_grad(noise, params, sequences, temperature: float, adjacency=None, 
 def compute_loss(noise, params, sequences, _metadata, temperature: float, adjacency, *,
                  graph_constraint_scale: float = 10.0, verbose: bool = False,
                  fix_seqs: bool = False, fix_tree: bool = False):
-    """Total loss (tree.py:299-361); ``noise`` replaces the PRNG key."""
+    """Total loss (tree.py:299-361); ``noise`` is a PRNGKey (split as the
+    reference splits its key) or update_tree's noise itself."""
     loss, _ = loss_and_grad(noise, params, sequences, temperature, adjacency,
                             graph_constraint_scale=graph_constraint_scale, fix_seqs=fix_seqs,
                             fix_tree=fix_tree)
