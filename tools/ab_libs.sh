@@ -14,6 +14,7 @@ if 'c4_shard' in d: extra += ' shard %.1f us' % d['c4_shard']['fused_kernel_us']
 if 'c2' in d: extra += ' c2 %.1f us' % (d['c2']['ms_per_step']*1e3)
 if 'c3' in d: extra += ' c3 soft %.1f us hard %.1f us' % (d['c3']['soft_ms_per_step']*1e3, d['c3']['hard_recon_ms_per_step']*1e3)
 if 'c5' in d: extra += ' c5 %.3f ms' % d['c5']['ms_per_step']
+if 'nk' in d: extra += ' nk_dna %.3f ms' % d['nk']['dna_256x2000_q4_k4']['ms_per_step']
 print(sys.argv[2], round(d['value']/1e9,1), d['roofline']['per_kernel_us'], extra)" gpurun_out/ab.json "$lib"
   done
 done
