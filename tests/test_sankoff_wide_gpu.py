@@ -309,15 +309,19 @@ def test_site_gate_repeat_calls_no_sync(device, tau, wide_kernel):
 
 
 @pytest.mark.parametrize("topo", ["balanced", "random"])
-@pytest.mark.parametrize("Q", [20, 13])
-def test_site_cherry_tables_are_bitwise_neutral(device, monkeypatch, topo, Q):
-    """The lane-per-site kernel's cherry tables (wide_dev.h site_pair_tables:
-    a height-1 row's forward message and softmin row sums by its children's
-    code pair, built by the gate) == the per-lane mat-vecs they replace
-    (TREX_SITE_CHERRY=0), bit for bit: DP table, scores, dC, marginals and
-    soft ancestral states, fused and separate launches, with missing leaf
-    states (code Q: the all-1e5 row's message) and cherries both under
-    height-2 rows and directly under task rows (random topologies)."""
+@pytest.mark.parametrize("knob,Q", [("TREX_SITE_CHERRY", 20), ("TREX_SITE_SROW", 20),
+                                    ("TREX_SITE_SROW", 13)])
+def test_site_kernel_shortcuts_are_bitwise_neutral(device, monkeypatch, topo, knob, Q):
+    """The lane-per-site kernel's two shortcuts are bitwise what they
+    replace: the cherry tables (wide_dev.h site_pair_tables: a height-1 row's
+    forward message and softmin row sums by its children's code pair, built
+    by the gate) == the per-lane mat-vecs (TREX_SITE_CHERRY=0, the Q = 20
+    build without tables), and the fused kernel's kept s rows (the forward's
+    K u of each computed child, re-read by the adjoint) == the adjoint's own
+    mat-vec (TREX_SITE_SROW=0): DP table, scores, dC, marginals and soft
+    ancestral states, fused and separate launches, with missing leaf states
+    (code Q: the all-1e5 row's message) and cherries both under height-2
+    rows and directly under task rows (random topologies)."""
     B, n, L, tau = 2, 64, 777, 0.5
     ch = (balanced_children(n, B) if topo == "balanced" else random_topologies(B, n, seed=71))
     leaves = random_leaves(B, n, L, Q, seed=72, missing=0.03)
@@ -325,7 +329,7 @@ def test_site_cherry_tables_are_bitwise_neutral(device, monkeypatch, topo, Q):
     lv, c = _dev(leaves, device), _dev(cost, device, torch.float32)
     runs = []
     for flag in ("1", "0"):
-        monkeypatch.setenv("TREX_SITE_CHERRY", flag)
+        monkeypatch.setenv(knob, flag)
         eng = _engine(ch, L, Q, device)
         f, dc, mg, an = eng.fwd_bwd(lv, c, tau, site_score=True, marginals=True,
                                     anc_states=True)

@@ -1377,6 +1377,9 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
       float* kg = reinterpret_cast<float*>(tail - 3456);  // K and K^T
       c.site_flag = flag;
       c.site_kg = kg;
+      if (phase == 3 && site_srow_on())
+        c.site_srow = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                               site_srow_offset(B, L, Q));
       if (int e = wide_run(fn, c, /*reduce=*/false)) return e;
       if (int e = site_run(fn, c, lanes, lp_slots, flag, kg)) return e;
       return partial_reduce(fn, static_cast<double*>(workspace),
@@ -1462,7 +1465,11 @@ extern "C" int trex_dp_site_major(int Q) {
 extern "C" int64_t trex_workspace_bytes(int B, int L, int n_all, int Q) {
   if (B <= 0 || L <= 0 || Q <= 0) return 0;
   if (Q > kWideMaxQ) return bigq_workspace_bytes(B, L, Q);
-  if (Q > 4) return wide_workspace_bytes(B, L, Q);
+  if (Q > kSiteMaxQ) return wide_workspace_bytes(B, L, Q);
+  if (Q > 4) {  // + the fused lane-per-site kernel's s rows
+    const int64_t ni = n_all - (n_all + 1) / 2;
+    return site_srow_offset(B, L, Q) + (int64_t)B * std::max<int64_t>(ni, 0) * L * Q * 4;
+  }
   const int64_t nb = (int64_t)B * tiles_for(L, 1);
   const int64_t narrow = counters_bytes(B) + nb * 8 * (1 + (int64_t)Q * Q) + (int64_t)Q * Q * B * 8 + 256;
   // small grids may run the state-parallel wide kernel (G = 4): room for both

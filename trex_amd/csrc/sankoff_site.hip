@@ -71,7 +71,8 @@ struct SiteArgs {
   double* part_dc;    // [Q * Q][B * tiles]
   const float* kg;    // K [kSQ][kSQ] and K^T (site_gate_write), zero-padded
   const float* ptab;  // cherry tables TM | TS (site_pair_tables), below K
-  int cherry;         // 0: no tables (TREX_SITE_CHERRY=0, A/B; bitwise the same)
+  int cherry;         // 0: the CH = false variants (TREX_SITE_CHERRY=0, A/B; bitwise the same)
+  float* srow;        // fused: s = K u of each computed internal child row, [B][n_int][L][Q]
   const int* flag;    // 1: this kernel handles the launch
   int n_slots;
 };
@@ -103,7 +104,9 @@ __device__ __forceinline__ int swz(int i, int s) { return i * kWave + (s ^ ((i &
 
 // QC: the alphabet size when it is 20 (C3: every state mask folds away), 0 =
 // runtime Q <= 20 with masked padded states
-template <int PHASE, int QC>
+// KS (fused only): keep the forward's s rows for the adjoint (A.srow);
+// CH: cherry tables (false: the per-lane mat-vecs, TREX_SITE_CHERRY=0 A/B)
+template <int PHASE, int QC, bool KS = false, bool CH = true>
 __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs A) {
   constexpr bool FWD = (PHASE & 1) != 0;
   constexpr bool BWD = (PHASE & 2) != 0;
@@ -208,6 +211,10 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
   const uint32_t rowbytes = (uint32_t)L * Q * 4;
   const uint32_t treebytes = (uint32_t)ni * rowbytes;
   const rsrc_t rdp = make_rsrc(A.dp + (size_t)tree * ni * L * Q, treebytes);
+  // fused calls keep each computed child row's s for the adjoint (the
+  // forward's mat-vec instead of a second one); srow null: recomputed
+  constexpr bool keep_s = FWD && BWD && KS;
+  const rsrc_t rsr = make_rsrc(keep_s ? A.srow + (size_t)tree * ni * L * Q : A.dp, treebytes);
   const int vbase = active ? site * Q * 4 : 0x7FFFFFF0;
   const bool q4 = (Q & 3) == 0;
   auto store_row = [&](rsrc_t r, int row, const float (&v)[kSQ]) {
@@ -225,12 +232,12 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         if (j < Q) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), r, vbase + 4 * j, row * rowbytes, 0);
     }
   };
-  auto load_row = [&](int row, float (&v)[kSQ]) {
+  auto load_row_r = [&](rsrc_t rr, int row, float (&v)[kSQ]) {
     if (q4) {
 #pragma unroll
       for (int c = 0; c < kSQ / 4; ++c) {
         u32x4 w = u32x4{0, 0, 0, 0};
-        if (4 * c < Q) w = __builtin_amdgcn_raw_buffer_load_b128(rdp, vbase + 16 * c, row * rowbytes, 1);
+        if (4 * c < Q) w = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 16 * c, row * rowbytes, 1);
         v[4 * c] = __uint_as_float(w.x);
         v[4 * c + 1] = __uint_as_float(w.y);
         v[4 * c + 2] = __uint_as_float(w.z);
@@ -239,10 +246,11 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     } else {
 #pragma unroll
       for (int j = 0; j < kSQ; ++j)
-        v[j] = j < Q ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rdp, vbase + 4 * j, row * rowbytes, 1))
+        v[j] = j < Q ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, vbase + 4 * j, row * rowbytes, 1))
                      : 0.0f;
     }
   };
+  auto load_row = [&](int row, float (&v)[kSQ]) { load_row_r(rdp, row, v); };
   auto slot_get = [&](int sl, float (&v)[kSQ]) {
 #pragma unroll
     for (int j = 0; j < kSQ; ++j) v[j] = slots[(size_t)sl * kSlotF + j * kWave + lane];
@@ -325,9 +333,11 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     wave_sync();
   };
   // message of a child with D = d to every parent state (sankoff.py:67-68, softmin)
-  auto message_add = [&](const float (&d)[kSQ], float (&dv)[kSQ], bool first) {
+  // srow_row >= 0 (fused, keep_s): the child's s row is stored for the adjoint
+  auto message_add = [&](const float (&d)[kSQ], float (&dv)[kSQ], bool first, int srow_row = -1) {
     float md, u[kSQ], s[kSQ];
     weights(d, md, u, s);
+    if (keep_s && srow_row >= 0) store_row(rsr, srow_row, s);
     const float base = md + cmin;
 #pragma unroll
     for (int i = 0; i < kSQ; ++i) {
@@ -370,7 +380,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         const int desc = c == 0 ? e.y : e.z;
         if (((desc >> 24) & 3) == kKindInline) {
           const I4 e2 = load_step(inl, desc & 0xFFFF);
-          if (A.cherry) {
+          if constexpr (CH) {
             cherry_add(e2, d, c == 0, store);
           } else {
             float dc[kSQ];
@@ -391,15 +401,15 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     if (kind == kKindInt) {
       float d[kSQ];
       slot_get((desc >> 16) & 0xFF, d);
-      message_add(d, dv, first);
+      message_add(d, dv, first, desc & 0xFFFF);
     } else if (kind == kKindInline) {
       const I4 e = load_step(inl, desc & 0xFFFF);
-      if (e.w <= 1 && A.cherry) {
+      if (CH && e.w <= 1) {
         cherry_add(e, dv, first, store);
       } else {
         float d[kSQ];
         inline_d(desc & 0xFFFF, d, store);
-        message_add(d, dv, first);
+        message_add(d, dv, first, e.x);
       }
     } else {
       leaf_add(desc, dv, first);
@@ -644,7 +654,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     // a cherry child: its row sums s from TS (the forward's mat-vec, bitwise)
     auto cherry_adj = [&](const I4& e, const float (&d)[kSQ], const float (&g)[kSQ],
                           float (&gc)[kSQ]) {
-      if (!A.cherry) {
+      if constexpr (!CH) {
         child_adj(d, g, gc);
         return;
       }
@@ -744,16 +754,27 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
           if (kind == kKindInt || kind == kKindInline) {
             const I4 ie = kind == kKindInline ? load_step(inl, desc & 0xFFFF) : I4{desc & 0xFFFF, 0, 0, 2};
             float d[kSQ], g[kSQ], gc[kSQ];
-            if (ie.w > 1)
+            if (ie.w > 1 && keep_s) {
+              // the forward's D and s rows of this child (no mat-vec)
+              float sv[kSQ], md, u[kSQ];
               load_row(ie.x, d);
-            else
-              cheap_d(ie, d);
-            slot_get(vslot, g);
-            if (c == 0) emit(stp.x & 0xFFFF, g);
-            if (ie.w > 1)
-              child_adj(d, g, gc);
-            else
-              cherry_adj(ie, d, g, gc);
+              weights_u(d, md, u);
+              load_row_r(rsr, ie.x, sv);
+              slot_get(vslot, g);
+              if (c == 0) emit(stp.x & 0xFFFF, g);
+              child_adj_rest(u, sv, g, gc);
+            } else {
+              if (ie.w > 1)
+                load_row(ie.x, d);
+              else
+                cheap_d(ie, d);
+              slot_get(vslot, g);
+              if (c == 0) emit(stp.x & 0xFFFF, g);
+              if (ie.w > 1)
+                child_adj(d, g, gc);
+              else
+                cherry_adj(ie, d, g, gc);
+            }
             if (kind == kKindInt)
               slot_put((desc >> 16) & 0xFF, gc);
             else
@@ -828,6 +849,11 @@ size_t site_lds_bytes(int n_slots, int nl, int ni) {
 
 // host-side eligibility (the cost-dependent mode is decided on the device):
 // soft, 4 < Q <= 20, every tree has a lane program whose slots fit the LDS
+bool site_srow_on() {
+  const char* e = std::getenv("TREX_SITE_SROW");  // "0": the adjoint recomputes s (A/B)
+  return !(e && e[0] == '0');
+}
+
 bool site_eligible(const WideCall& c, int lp_slots) {
   if (!c.soft || c.Q <= 4 || c.Q > kSQ || lp_slots < 0) return false;
   const char* e = std::getenv("TREX_SITE");  // "0": the state-parallel kernel (A/B)
@@ -866,6 +892,7 @@ int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slo
   A.part_dc = A.part_tree + nb;
   A.kg = kg;
   A.ptab = kg - kSiteTabBytes / 4;
+  A.srow = c.phase == 3 ? c.site_srow : nullptr;
   {
     const char* e = std::getenv("TREX_SITE_CHERRY");  // read per call (tests flip it)
     A.cherry = !(e && e[0] == '0');
@@ -877,11 +904,21 @@ int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slo
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kernel, dim3((int)nb), dim3(kSWv * kWave), lds, st, A);
   };
-  if (c.Q == kSQ) {
+  const bool ks = A.srow != nullptr;
+  if (c.Q == kSQ && !A.cherry) {  // A/B: no cherry tables, no kept s rows
+    if (c.phase == 1)
+      go(sankoff_site_kernel<1, kSQ, false, false>);
+    else if (c.phase == 2)
+      go(sankoff_site_kernel<2, kSQ, false, false>);
+    else
+      go(sankoff_site_kernel<3, kSQ, false, false>);
+  } else if (c.Q == kSQ) {
     if (c.phase == 1)
       go(sankoff_site_kernel<1, kSQ>);
     else if (c.phase == 2)
       go(sankoff_site_kernel<2, kSQ>);
+    else if (ks)
+      go(sankoff_site_kernel<3, kSQ, true>);
     else
       go(sankoff_site_kernel<3, kSQ>);
   } else {
@@ -889,6 +926,8 @@ int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slo
       go(sankoff_site_kernel<1, 0>);
     else if (c.phase == 2)
       go(sankoff_site_kernel<2, 0>);
+    else if (ks)
+      go(sankoff_site_kernel<3, 0, true>);
     else
       go(sankoff_site_kernel<3, 0>);
   }

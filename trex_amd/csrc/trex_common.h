@@ -114,6 +114,10 @@ struct WideCall {
   // its K / K^T (site_kg) and the flag (site_flag) from workgroup 0
   int* site_flag = nullptr;
   float* site_kg = nullptr;
+  // fused site kernel: its forward's softmin row sums s = K u of every
+  // internal child row it computes, re-read by its adjoint (workspace past
+  // the wide workspace, DP-table layout; null: recomputed)
+  float* site_srow = nullptr;
 };
 constexpr int kWideMaxQ = 64;
 // 64 < Q <= 128: the large-alphabet kernel (sankoff_bigq.hip; int8 leaf codes
@@ -156,6 +160,11 @@ int wide_ragged_run(const char* fn, const WideCall& c, const int* rmeta, const i
                     int64_t items);
 // lane-per-site kernel for the factored softmin, 4 < Q <= 20 (sankoff_site.hip)
 bool site_eligible(const WideCall& c, int lp_slots);
+constexpr int kSiteMaxQ = 20;  // the lane-per-site kernel's largest Q (kSiteSQ, wide_dev.h)
+bool site_srow_on();  // TREX_SITE_SROW != "0" (read per call)
+inline int64_t site_srow_offset(int B, int L, int Q) {
+  return (wide_workspace_bytes(B, L, Q) + 255) / 256 * 256;
+}
 int site_tiles(int L);
 int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots,
              const int* flag, const float* kg);
