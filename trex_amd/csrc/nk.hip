@@ -569,7 +569,7 @@ __device__ __forceinline__ void nk_fwd_loop(float (&f)[PPL][K][Q], cptr<float> F
   if constexpr (J >= K - 2) {
     nk_fwd_body<Q, K, PPL>(f, F, acc);
   } else {
-    constexpr int step = nk_cpow(Q, K - 1 - J) * Q;  // F entries per digit-J value
+    constexpr int step = nk_cpow(Q, K - 1 - J);  // F entries per digit-J value
 #pragma unroll 1
     for (int d = 0; d < Q; ++d) {
       nk_fwd_loop<Q, K, PPL, J + 1>(f, F + d * step, acc);
@@ -659,7 +659,7 @@ __device__ __forceinline__ void nk_bwd_loop(float (&f)[PPL][K][Q], const float (
   if constexpr (J >= K - 2) {
     nk_bwd_body<Q, K, PPL>(f, gs, F, gb);
   } else {
-    constexpr int step = nk_cpow(Q, K - 1 - J) * Q;
+    constexpr int step = nk_cpow(Q, K - 1 - J);
 #pragma unroll 1
     for (int d = 0; d < Q; ++d) {
       nk_bwd_loop<Q, K, PPL, J + 1>(f, gs, F + d * step, gb);
