@@ -93,13 +93,15 @@ def sankoff_fwd_bwd_ref(children, leaves, cost, tau, d_tree_score=1.0,
     tree_score, d_cost (Q, Q), marginals (n_int, Q, L), and dp_mag
     (n_int, Q, L), each D entry's error scale for an fp32 evaluation:
 
-        Dmag_v[i] = sum_c (|C_ij*| + tau log s_c[i] + Dmag_c*),
+        Dmag_v[i] = sum_c (|C_ij*| + tau (log s_c[i] + 1) + Dmag_c*),
 
     j* = argmin_j (C_ij + D_c[j]), s_c[i] = sum_j exp(-(x_j - min x) / tau),
     Dmag_c* = sum_j w_c[i, j] Dmag_c[j] for an internal child, |D_c[j*]| for
     a leaf / 1e5 row (exact inputs; 1e5 for a missing state).  This is the
     running error bound of the recursion -- D evaluated with every term's
-    magnitude (M_c[i] = C_ij* + D_c[j*] - tau log s_c[i]; a softmin is
+    magnitude (M_c[i] = C_ij* + D_c[j*] - tau log s_c[i]; s >= 1 is a sum
+    rounded relative to itself, so tau log s carries an absolute error of
+    order tau eps even where log s ~ 0: hence tau (log s + 1); a softmin is
     1-Lipschitz, so the child's error arrives weighted by w).  A D entry that
     sums messages of either sign to ~0 keeps the absolute scale of its terms.
     """
@@ -122,7 +124,9 @@ def sankoff_fwd_bwd_ref(children, leaves, cost, tau, d_tree_score=1.0,
             acc = acc + M
             js = np.argmin(x, axis=-1)  # (L, Qi)
             xm = np.take_along_axis(x, js[..., None], axis=-1)[..., 0]
-            mag = mag + np.abs(cost[np.arange(Q)[None, :], js]) + (xm - M)  # xm - M = tau log s
+            # xm - M = tau log s; + tau: s >= 1 carries a relative rounding,
+            # i.e. tau log s an absolute one of ~tau eps (log s ~ 0 included)
+            mag = mag + np.abs(cost[np.arange(Q)[None, :], js]) + (xm - M) + tau
             if kind == "int":
                 mag = mag + np.einsum("lij,lj->li", w, Dmag[idx])
             else:

@@ -28,7 +28,7 @@ for step in "$@"; do
   echo "[gpu_run] $TAG $name $arg"
   case "$name" in
     suite)
-      timeout -k 10 900 python -u -m pytest ${arg:-tests} -m gpu -x -q --timeout 120 \
+      timeout -k 10 900 python -u -m pytest ${arg:-tests} -m gpu --maxfail=5 -q --timeout 120 \
         --timeout-method thread > "$OUT/${TAG}_suite.log" 2>&1 || { tail -30 "$OUT/${TAG}_suite.log"; exit 1; }
       tail -3 "$OUT/${TAG}_suite.log" ;;
     smoke)
