@@ -760,6 +760,9 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
               load_row(ie.x, d);
               weights_u(d, md, u);
               load_row_r(rsr, ie.x, sv);
+              // lanes past L read 0 (their g is 0): keep r = g / s finite
+#pragma unroll
+              for (int i = 0; i < kSQ; ++i) sv[i] = active ? sv[i] : 1.0f;
               slot_get(vslot, g);
               if (c == 0) emit(stp.x & 0xFFFF, g);
               child_adj_rest(u, sv, g, gc);
