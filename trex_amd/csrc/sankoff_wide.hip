@@ -380,7 +380,7 @@ __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_
       if (blockIdx.x == 0) site_gate_write(A.cost, Q, gmin, A.a, A.site_kg, A.site_flag, handled);
       if (handled) {
         // the first workgroups build the cherry tables below K
-        __shared__ float kl[kSiteSQ * kSiteSQ];
+        __shared__ float kl[kSiteSQ * kSiteSQ + kSiteSQ];
         site_pair_tables(A.cost, Q, gmin, A.a, A.bcoef, A.site_kg - kSiteTabBytes / 4, kl);
         return;
       }

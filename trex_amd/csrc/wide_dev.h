@@ -171,49 +171,54 @@ __device__ __forceinline__ int site_pair(int c0, int c1) {
   const int lo = c0 < c1 ? c0 : c1, hi = c0 < c1 ? c1 : c0;
   return hi * (hi + 1) / 2 + lo;
 }
-// the workgroups of the gate share the pairs (64 per workgroup and round);
-// kl: [kSiteSQ * kSiteSQ] floats of LDS for this workgroup's copy of K
+// one (pair, state) entry per thread: the workgroups of the gate share the
+// (Q + 1)(Q + 2) / 2 * 20 entries (64 per workgroup and round, 73
+// workgroups at Q = 20), each thread recomputing its pair's D and u (20
+// values) and its own row sum s_i -- a few hundred instructions, so the
+// gate launch the site kernel waits on stays short.  kl: [kSiteSQ *
+// kSiteSQ + kSiteSQ] floats of LDS (this workgroup's K, then T[Q])
 __device__ __forceinline__ void site_pair_tables(const float* cost, int Q, float cmin, float a,
                                                  float bcoef, float* tm, float* kl) {
   const int lane = threadIdx.x & (kWave - 1);
-  if ((int)blockIdx.x * kWave >= kSitePairs) return;
+  constexpr int kEntries = kSitePairs * kSiteSQ;
+  if ((int)blockIdx.x * kWave >= kEntries) return;
   for (int e = lane; e < kSiteSQ * kSiteSQ; e += kWave) {
     const int i = e / kSiteSQ, j = e - i * kSiteSQ;
     kl[e] = (i < Q && j < Q) ? fast_exp2((cmin - cost[i * Q + j]) * a) : 0.0f;
   }
   __syncthreads();
+  float* tq = kl + kSiteSQ * kSiteSQ;  // T[Q][i]: the all-1e5 row's message
+  if (lane < kSiteSQ) {
+    float sk = 0.0f;
+    for (int j = 0; j < Q; ++j) sk += kl[lane * kSiteSQ + j];
+    tq[lane] = lane < Q ? fmaf(-bcoef, fast_log2(sk), kSentinel + cmin) : 0.0f;
+  }
+  __syncthreads();
   float* ts = tm + kSitePairs * kSiteSQ;
-  for (int p = (int)blockIdx.x * kWave + lane; p < kSitePairs; p += (int)gridDim.x * kWave) {
+  for (int t = (int)blockIdx.x * kWave + lane; t < kEntries; t += (int)gridDim.x * kWave) {
+    const int p = t / kSiteSQ, i = t - p * kSiteSQ;
     int hi = 0;
     while ((hi + 1) * (hi + 2) / 2 <= p) ++hi;
     const int lo = p - hi * (hi + 1) / 2;
     if (hi > Q) continue;  // codes are 0..Q
-    // T[c][i] as the site kernel's prologue builds it (sankoff_site.hip)
-    auto trow = [&](int code, int i) -> float {
-      if (i >= Q) return 0.0f;
-      if (code < Q) return cost[i * Q + code];
-      float sk = 0.0f;
-      for (int j = 0; j < Q; ++j) sk += kl[i * kSiteSQ + j];
-      return fmaf(-bcoef, fast_log2(sk), kSentinel + cmin);
+    // T[c][j] as the site kernel's prologue builds it (sankoff_site.hip)
+    auto trow = [&](int code, int j) -> float {
+      return j >= Q ? 0.0f : code < Q ? cost[j * Q + code] : tq[j];
     };
-    float d[kSiteSQ], u[kSiteSQ];
+    float d[kSiteSQ];
 #pragma unroll
-    for (int i = 0; i < kSiteSQ; ++i) d[i] = trow(lo, i) + trow(hi, i);
+    for (int j = 0; j < kSiteSQ; ++j) d[j] = trow(lo, j) + trow(hi, j);
     float md = d[0];
 #pragma unroll
     for (int j = 1; j < kSiteSQ; ++j) md = j < Q ? fminf(md, d[j]) : md;
     const float mda = md * a;
+    float sv = 0.0f;
 #pragma unroll
-    for (int j = 0; j < kSiteSQ; ++j) u[j] = j < Q ? fast_exp2(fmaf(-d[j], a, mda)) : 0.0f;
-    const float base = md + cmin;
-#pragma unroll
-    for (int i = 0; i < kSiteSQ; ++i) {
-      float s = 0.0f;
-      for (int j = 0; j < Q; ++j) s = fmaf(kl[i * kSiteSQ + j], u[j], s);
-      s = i < Q ? s : 1.0f;
-      ts[p * kSiteSQ + i] = s;
-      tm[p * kSiteSQ + i] = i < Q ? fmaf(-bcoef, fast_log2(s), base) : 0.0f;
-    }
+    for (int j = 0; j < kSiteSQ; ++j)
+      if (j < Q) sv = fmaf(kl[i * kSiteSQ + j], fast_exp2(fmaf(-d[j], a, mda)), sv);
+    sv = i < Q ? sv : 1.0f;
+    ts[t] = sv;
+    tm[t] = i < Q ? fmaf(-bcoef, fast_log2(sv), md + cmin) : 0.0f;
   }
 }
 
