@@ -215,40 +215,89 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
   // forward's mat-vec instead of a second one); srow null: recomputed
   constexpr bool keep_s = FWD && BWD && KS;
   const rsrc_t rsr = make_rsrc(keep_s ? A.srow + (size_t)tree * ni * L * Q : A.dp, treebytes);
-  const int vbase = active ? site * Q * 4 : 0x7FFFFFF0;
   const bool q4 = (Q & 3) == 0;
+  // Row I/O through the wave's scratch (xr): a lane's Q values are 4Q
+  // bytes apart from its neighbour's in the site-major row, so a direct
+  // 16-B-per-lane access touches 5x the cache lines of a contiguous one
+  // (C3: a workgroup's forward stage 0 at 45 k cycles of which 21 k were the
+  // strided stores; lane-contiguous, 24 k).  The tile's row block (64 sites
+  // x Q floats, contiguous in HBM) is instead transposed in LDS: lane l
+  // moves bytes [16 (l + 64 c), +16) -- every wave instruction 1 KiB
+  // contiguous.  Bytes of sites past L are skipped (stores) / read as 0.
+  const int tb = tile * kWave * Q * 4;  // this tile's first byte in a row
+  const int tbytes = (min(L, (tile + 1) * kWave) - tile * kWave) * Q * 4;
   auto store_row = [&](rsrc_t r, int row, const float (&v)[kSQ]) {
+#ifdef SITE_DIAG_NOSTORE  // diagnostic: no row stores (wrong results)
+    return;
+#endif
     if (q4) {
 #pragma unroll
       for (int c = 0; c < kSQ / 4; ++c)
         if (4 * c < Q)
+          *reinterpret_cast<float4*>(xr + lane * Q + 4 * c) =
+              make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+      wave_sync();
+#pragma unroll
+      for (int c = 0; c < kSQ / 4; ++c) {
+        if (4 * c < Q) {
+          const int o = 16 * (lane + kWave * c);
+          const float4 w = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(xr) + o);
           __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4{__float_as_uint(v[4 * c]), __float_as_uint(v[4 * c + 1]), __float_as_uint(v[4 * c + 2]),
-                    __float_as_uint(v[4 * c + 3])},
-              r, vbase + 16 * c, row * rowbytes, 0);
+              u32x4{__float_as_uint(w.x), __float_as_uint(w.y), __float_as_uint(w.z), __float_as_uint(w.w)},
+              r, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 0);
+        }
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < kSQ; ++j)
-        if (j < Q) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), r, vbase + 4 * j, row * rowbytes, 0);
+        if (j < Q) xr[lane * Q + j] = v[j];
+      wave_sync();
+#pragma unroll
+      for (int j = 0; j < kSQ; ++j) {
+        if (j < Q) {
+          const int o = 4 * (lane + kWave * j);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xr[lane + kWave * j]), r,
+                                                o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 0);
+        }
+      }
     }
+    wave_sync();
   };
   auto load_row_r = [&](rsrc_t rr, int row, float (&v)[kSQ]) {
     if (q4) {
 #pragma unroll
       for (int c = 0; c < kSQ / 4; ++c) {
-        u32x4 w = u32x4{0, 0, 0, 0};
-        if (4 * c < Q) w = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 16 * c, row * rowbytes, 1);
-        v[4 * c] = __uint_as_float(w.x);
-        v[4 * c + 1] = __uint_as_float(w.y);
-        v[4 * c + 2] = __uint_as_float(w.z);
-        v[4 * c + 3] = __uint_as_float(w.w);
+        if (4 * c < Q) {
+          const int o = 16 * (lane + kWave * c);
+          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rr, o < tbytes ? tb + o : 0x7FFFFFF0,
+                                                               row * rowbytes, 1);
+          *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(xr) + o) = w;
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int c = 0; c < kSQ / 4; ++c) {
+        float4 w = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (4 * c < Q) w = *reinterpret_cast<const float4*>(xr + lane * Q + 4 * c);
+        v[4 * c] = w.x;
+        v[4 * c + 1] = w.y;
+        v[4 * c + 2] = w.z;
+        v[4 * c + 3] = w.w;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < kSQ; ++j)
-        v[j] = j < Q ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, vbase + 4 * j, row * rowbytes, 1))
-                     : 0.0f;
+      for (int j = 0; j < kSQ; ++j) {
+        if (j < Q) {
+          const int o = 4 * (lane + kWave * j);
+          xr[lane + kWave * j] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rr, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 1));
+        }
+      }
+      wave_sync();
+#pragma unroll
+      for (int j = 0; j < kSQ; ++j) v[j] = j < Q ? xr[lane * Q + j] : 0.0f;
     }
+    wave_sync();
   };
   auto load_row = [&](int row, float (&v)[kSQ]) { load_row_r(rdp, row, v); };
   auto slot_get = [&](int sl, float (&v)[kSQ]) {
