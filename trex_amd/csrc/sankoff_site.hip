@@ -224,6 +224,8 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
   // x Q floats, contiguous in HBM) is instead transposed in LDS: lane l
   // moves bytes [16 (l + 64 c), +16) -- every wave instruction 1 KiB
   // contiguous.  Bytes of sites past L are skipped (stores) / read as 0.
+  // the transposes' own ordering point: all of this wave's LDS traffic done
+  auto lds_sync = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   const int tb = tile * kWave * Q * 4;  // this tile's first byte in a row
   const int tbytes = (min(L, (tile + 1) * kWave) - tile * kWave) * Q * 4;
   auto store_row = [&](rsrc_t r, int row, const float (&v)[kSQ]) {
@@ -236,22 +238,29 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         if (4 * c < Q)
           *reinterpret_cast<float4*>(xr + lane * Q + 4 * c) =
               make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
-      wave_sync();
+      lds_sync();
+      u32x4 w[kSQ / 4];
+#pragma unroll
+      for (int c = 0; c < kSQ / 4; ++c)
+        if (4 * c < Q)
+          w[c] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(xr) + 16 * (lane + kWave * c));
 #pragma unroll
       for (int c = 0; c < kSQ / 4; ++c) {
         if (4 * c < Q) {
           const int o = 16 * (lane + kWave * c);
-          const float4 w = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(xr) + o);
-          __builtin_amdgcn_raw_buffer_store_b128(
-              u32x4{__float_as_uint(w.x), __float_as_uint(w.y), __float_as_uint(w.z), __float_as_uint(w.w)},
-              r, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(w[c], r, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 0);
         }
       }
+      // the stores' data registers stay untouched past the last store's issue
+      // (without this the compiler reused the last chunk's registers for the
+      // next VALU result right after the store and a few lanes' bytes landed
+      // corrupted; observed on MI355X, tools/dbg/site_dp2.py)
+      asm volatile("s_nop 4" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]));
     } else {
 #pragma unroll
       for (int j = 0; j < kSQ; ++j)
         if (j < Q) xr[lane * Q + j] = v[j];
-      wave_sync();
+      lds_sync();
 #pragma unroll
       for (int j = 0; j < kSQ; ++j) {
         if (j < Q) {
@@ -261,7 +270,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         }
       }
     }
-    wave_sync();
+    lds_sync();
   };
   auto load_row_r = [&](rsrc_t rr, int row, float (&v)[kSQ]) {
     if (q4) {
@@ -274,7 +283,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
           *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(xr) + o) = w;
         }
       }
-      wave_sync();
+      lds_sync();
 #pragma unroll
       for (int c = 0; c < kSQ / 4; ++c) {
         float4 w = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -293,11 +302,11 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
               __builtin_amdgcn_raw_buffer_load_b32(rr, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 1));
         }
       }
-      wave_sync();
+      lds_sync();
 #pragma unroll
       for (int j = 0; j < kSQ; ++j) v[j] = j < Q ? xr[lane * Q + j] : 0.0f;
     }
-    wave_sync();
+    lds_sync();
   };
   auto load_row = [&](int row, float (&v)[kSQ]) { load_row_r(rdp, row, v); };
   auto slot_get = [&](int sl, float (&v)[kSQ]) {
