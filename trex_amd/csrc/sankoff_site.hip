@@ -272,7 +272,43 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     }
     lds_sync();
   };
-  auto load_row_r = [&](rsrc_t rr, int row, float (&v)[kSQ]) {
+  // direct (lane-strided) row I/O: the loads stay asynchronous (the wave
+  // waits only where it uses the values)
+  const int vbase = active ? site * Q * 4 : 0x7FFFFFF0;
+  auto store_row_direct = [&](rsrc_t r, int row, const float (&v)[kSQ]) {
+    if (q4) {
+#pragma unroll
+      for (int c = 0; c < kSQ / 4; ++c)
+        if (4 * c < Q)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{__float_as_uint(v[4 * c]), __float_as_uint(v[4 * c + 1]), __float_as_uint(v[4 * c + 2]),
+                    __float_as_uint(v[4 * c + 3])},
+              r, vbase + 16 * c, row * rowbytes, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSQ; ++j)
+        if (j < Q) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), r, vbase + 4 * j, row * rowbytes, 0);
+    }
+  };
+  auto load_row_direct = [&](rsrc_t rr, int row, float (&v)[kSQ]) {
+    if (q4) {
+#pragma unroll
+      for (int c = 0; c < kSQ / 4; ++c) {
+        u32x4 w = u32x4{0, 0, 0, 0};
+        if (4 * c < Q) w = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 16 * c, row * rowbytes, 1);
+        v[4 * c] = __uint_as_float(w.x);
+        v[4 * c + 1] = __uint_as_float(w.y);
+        v[4 * c + 2] = __uint_as_float(w.z);
+        v[4 * c + 3] = __uint_as_float(w.w);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSQ; ++j)
+        v[j] = j < Q ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, vbase + 4 * j, row * rowbytes, 1))
+                     : 0.0f;
+    }
+  };
+  auto load_row_t = [&](rsrc_t rr, int row, float (&v)[kSQ]) {
     if (q4) {
 #pragma unroll
       for (int c = 0; c < kSQ / 4; ++c) {
@@ -307,6 +343,15 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
       for (int j = 0; j < kSQ; ++j) v[j] = j < Q ? xr[lane * Q + j] : 0.0f;
     }
     lds_sync();
+  };
+#ifndef SITE_LOAD_T
+#define SITE_LOAD_T 0  // transposed (synchronous) row loads: slower in the adjoint (PERFLOG)
+#endif
+  auto load_row_r = [&](rsrc_t rr, int row, float (&v)[kSQ]) {
+    if (SITE_LOAD_T)
+      load_row_t(rr, row, v);
+    else
+      load_row_direct(rr, row, v);
   };
   auto load_row = [&](int row, float (&v)[kSQ]) { load_row_r(rdp, row, v); };
   auto slot_get = [&](int sl, float (&v)[kSQ]) {
@@ -734,8 +779,16 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     const bool want_marg = A.marg != nullptr;
     const rsrc_t rmg = make_rsrc(want_marg ? A.marg + (size_t)tree * ni * L * Q : A.dp, treebytes);
     int8_t* at = A.anc ? A.anc + (size_t)tree * ni * L + site : nullptr;
+#ifndef SITE_EMIT_T
+#define SITE_EMIT_T 0  // 1: marginal rows through the transposed store (slower, PERFLOG)
+#endif
     auto emit = [&](int row, const float (&g)[kSQ]) {
-      if (want_marg) store_row(rmg, row, g);
+      if (want_marg) {
+        if (SITE_EMIT_T)
+          store_row(rmg, row, g);
+        else
+          store_row_direct(rmg, row, g);
+      }
       if (at && active) {
         float bv = g[0];
         int bi = 0;
