@@ -315,3 +315,28 @@ def test_register_kernels_bitwise_the_rolled_kernels(device, monkeypatch, Q, k):
                                         NK.NKLandscape(c["inter"][:64] % 64, c["F"][:64], Q,
                                                        device), k))
     np.testing.assert_allclose(got, ref, rtol=RTOL, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["split_x3", "split_f32", "whole"])
+def test_landscape_loss_surrogate_paths_vs_oracle(device, monkeypatch, mode):
+    """The NK loss's surrogate as the C5 step runs it (leaf x leaf Gram block
+    cached, d surrogate / dS for the ancestor rows only; f16x3 split GEMMs
+    when K % 16 == 0, f32 with TREX_NK_X3=0) and trex_tree_surrogate's
+    all-rows path (TREX_NK_SPLIT=0), each vs the fp64 oracle at a DNA-like
+    shape: loss at rtol 1e-5, d ancestors per entry (landscape_grad_bound)."""
+    monkeypatch.setenv("TREX_NK_SPLIT", "0" if mode == "whole" else "1")
+    monkeypatch.setenv("TREX_NK_X3", "0" if mode == "split_f32" else "1")
+    c = _case(128, 200, 4, 4, seed=17, mask=True)
+    land = NK.NKLandscape(c["inter"], c["F"], 4, device)
+    fn = NK.LandscapeAwareLoss(c["A"], 128, land, 0.9, 4, seq_mask=c["mask"])
+    assert fn.split == (mode != "whole") and (mode == "whole" or fn.x3 == (mode == "split_x3"))
+    s = torch.as_tensor(c["S0"], device=device)
+    for step in range(2):  # the second call reuses the cached leaf x leaf block
+        anc = c["anc"] * (1.0 + 0.1 * step)
+        loss, g = fn.value_and_grad(torch.as_tensor(anc, device=device), s)
+        args = (anc.astype(np.float64), c["S0"].astype(np.float64), 128, c["inter"],
+                c["F"].astype(np.float64), c["A"], 0.9, 4, 1.0, c["mask"])
+        rl, rg = nk.landscape_loss_grad(*args)
+        np.testing.assert_allclose(float(loss[0]), rl, rtol=RTOL)
+        assert_bound_close(_n(g), rg, landscape_grad_bound(*args, rtol=RTOL),
+                           what=f"{mode} step {step}")

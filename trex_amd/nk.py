@@ -21,6 +21,8 @@ rows, :286) and the inverse-interaction lists are built once on the host.
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 from ._lib import check, lib, ptr, stream_handle
@@ -151,6 +153,22 @@ class LandscapeAwareLoss:
                                    dtype=torch.uint8, device=dev)
         nb = int(L_.trex_nk_workspace_bytes(self.N, self.L, self.Q, k, self.n_parents))
         self.nk_ws = torch.empty(max(nb, 256), dtype=torch.uint8, device=dev)
+        # the surrogate as the C5 step runs it (TreeOptimizer): the leaf x leaf
+        # block of the Gram is data (computed when the leaves change, skipped
+        # per call), and d surrogate / dS only for the ancestor rows (the
+        # leaf rows of dS are never used: leaves are fixed data) -- f16x3
+        # split-product MFMA GEMMs when K % 16 == 0 (|S| <= 1, |M| <= m_bound:
+        # their contract), f32 MFMA otherwise.  Small problems keep
+        # trex_tree_surrogate's one-launch kernel (N <= 64, N K <= 4096).
+        self.split = not (self.N <= 64 and self.N * K <= 4096) and \
+            os.environ.get("TREX_NK_SPLIT", "1") != "0"
+        if self.split:
+            self.x3 = K % 16 == 0 and os.environ.get("TREX_NK_X3", "1") != "0"
+            self.G = torch.empty((self.N, self.N), **f32)
+            self.M = torch.empty((self.N, self.N), **f32)
+            self.m_bound = float(np.abs(A).sum(0).max() + np.abs(A).sum(1).max()
+                                 + 2.0 * np.abs(A).max()) + 1.0
+            self.dS_sur[: self.n_leaves].zero_()  # never written: the leaf rows' dS is unused
 
     def value_and_grad(self, ancestors, masked_sequences, *, want_grad: bool = True, out=None,
                        refresh: bool = False):
@@ -190,16 +208,39 @@ class LandscapeAwareLoss:
         if refresh or ms is not self._s_src or ver is None or ver != self._s_ver:
             self.S.copy_(ms)
             self._s_src, self._s_ver = ms, ver
+            if self.split:  # the leaf x leaf Gram block of these leaves
+                check(lib().trex_tree_gram(ptr(self.S), self.N, self.L * self.Q, ptr(self.G),
+                                           ptr(self.tree_ws), self.tree_ws.numel(),
+                                           stream_handle(self.S.device)))
 
     def _loss_and_dS(self, want_grad: bool):
         """Loss and d loss / d S (all rows) of the current S."""
         L_ = lib()
         st = stream_handle(self.S.device)
         K = self.L * self.Q
-        check(L_.trex_tree_surrogate(ptr(self.S), ptr(self.A), self.N, K, ptr(self.sur),
-                                     ptr(self.dS_sur) if want_grad else None,
-                                     ptr(self.dA) if want_grad else None, None,
-                                     ptr(self.tree_ws), self.tree_ws.numel(), st))
+        N, nl = self.N, self.n_leaves
+        if self.split:
+            ws, wsb = ptr(self.tree_ws), self.tree_ws.numel()
+            if self.x3:
+                check(L_.trex_tree_gram_skip_x3(ptr(self.S), N, K, nl, 1.0, ptr(self.G), ws, wsb,
+                                                st))
+            else:
+                check(L_.trex_tree_gram_skip(ptr(self.S), N, K, nl, ptr(self.G), ws, wsb, st))
+            check(L_.trex_tree_surrogate_combine(ptr(self.A), ptr(self.G), N, ptr(self.sur),
+                                                 ptr(self.dA), ptr(self.M), ws, st))
+            if want_grad:
+                dS = ptr(self.dS_sur[nl:])
+                if self.x3:
+                    check(L_.trex_tree_mf_rows_x3(ptr(self.M), ptr(self.S), N, K, nl, N - nl,
+                                                  self.m_bound, 1.0, dS, st))
+                else:
+                    check(L_.trex_tree_mf_rows(ptr(self.M), ptr(self.S), N, K, nl, N - nl, dS,
+                                               st))
+        else:
+            check(L_.trex_tree_surrogate(ptr(self.S), ptr(self.A), N, K, ptr(self.sur),
+                                         ptr(self.dS_sur) if want_grad else None,
+                                         ptr(self.dA) if want_grad else None, None,
+                                         ptr(self.tree_ws), self.tree_ws.numel(), st))
         if self.fitness_on:
             check(L_.trex_nk_landscape_loss(
                 ptr(self.plan), self.n_parents, ptr(self.S), self.N, self.L, self.Q,
