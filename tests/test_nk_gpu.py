@@ -317,6 +317,25 @@ def test_register_kernels_bitwise_the_rolled_kernels(device, monkeypatch, Q, k):
     np.testing.assert_allclose(got, ref, rtol=RTOL, atol=1e-6)
 
 
+@pytest.mark.parametrize("k,mask", [(1, False), (2, True), (4, True)])
+def test_q4_vector_kernels_bitwise_the_generic_kernels(device, monkeypatch, k, mask):
+    """Q = 4's float4 cross-entropy / combine kernels (csrc/nk.hip nk_ce4_kernel,
+    nk_combine4_kernel) == the generic per-state kernels (TREX_NK_V4=0) bit for
+    bit: loss and d ancestors, with and without the site mask."""
+    c = _case(64, 300, 4, k, seed=40 + k, mask=mask)
+    land = NK.NKLandscape(c["inter"], c["F"], 4, device)
+    a = torch.as_tensor(c["anc"], device=device)
+    s = torch.as_tensor(c["S0"], device=device)
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TREX_NK_V4", flag)
+        fn = NK.LandscapeAwareLoss(c["A"], 64, land, 0.7, k, seq_mask=c["mask"] if mask else None)
+        loss, g = fn.value_and_grad(a, s)
+        torch.cuda.synchronize()
+        runs.append((loss.clone(), g.clone()))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+
+
 @pytest.mark.parametrize("mode", ["split_x3", "split_f32", "whole"])
 def test_landscape_loss_surrogate_paths_vs_oracle(device, monkeypatch, mode):
     """The NK loss's surrogate as the C5 step runs it (leaf x leaf Gram block

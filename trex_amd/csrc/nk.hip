@@ -786,6 +786,57 @@ __global__ __launch_bounds__(256) void nk_ce_kernel(const float* __restrict__ S,
   }
 }
 
+// Q = 4: the same cross-entropy with one 16-B access per row (float4 logits,
+// child rows, d child, d logits) instead of four strided dwords -- the
+// arithmetic of nk_ce_one step for step (bitwise the generic kernel)
+__global__ __launch_bounds__(256) void nk_ce4_kernel(const float4* __restrict__ S,
+                                                     const float4* __restrict__ logits,
+                                                     const int32_t* __restrict__ cofs,
+                                                     const int32_t* __restrict__ cidx,
+                                                     const float* __restrict__ mask, int nP, int L,
+                                                     float scale, float4* __restrict__ dlog,
+                                                     float4* __restrict__ dchild,
+                                                     double* __restrict__ part) {
+  const int64_t total = (int64_t)nP * L;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int pc = (int)(t / L), l = (int)(t - (int64_t)pc * L);
+    const float4 x4 = logits[t];
+    const float xv[4] = {x4.x, x4.y, x4.z, x4.w};
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) mx = fmaxf(mx, xv[s]);
+    float se = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) se += expf(xv[s] - mx);
+    const float lse = mx + logf(se);
+    const float mk = mask ? mask[l] : 1.0f;
+    float dl[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    double ce = 0.0;
+    for (int e = cofs[pc]; e < cofs[pc + 1]; ++e) {
+      const size_t row = (size_t)cidx[e] * L + l;
+      const float4 v4 = S[row];
+      const float sv[4] = {v4.x, v4.y, v4.z, v4.w};
+      float tot = 0.0f, cen = 0.0f, dcv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float lp = xv[s] - lse;
+        tot += sv[s];
+        cen -= sv[s] * lp;
+        dcv[s] = -scale * mk * lp;
+        dl[s] -= sv[s];
+      }
+      dchild[row] = make_float4(dcv[0], dcv[1], dcv[2], dcv[3]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dl[s] += expf(xv[s] - lse) * tot;
+      ce += (double)(mk * cen);
+    }
+    dlog[t] = make_float4(scale * mk * dl[0], scale * mk * dl[1], scale * mk * dl[2],
+                          scale * mk * dl[3]);
+    part[t] = ce;
+  }
+}
+
 // fixed-order two-level sum of the CE partials: block b sums chunk b into
 // sums[b]; nk_loss_kernel then sums the chunks and writes
 // loss = surrogate + lambda * ce / norm
@@ -850,6 +901,42 @@ __global__ __launch_bounds__(256) void nk_combine_kernel(const float* __restrict
           acc += G[((size_t)pc * L * k + ient[e]) * Q + q];
       }
       v += acc;
+    }
+    dout[t] = v;
+  }
+}
+
+// Q = 4: one thread per (node, site) row, float4 rows and gathers (the
+// generic kernel's per-state sums in the same order: bitwise)
+__global__ __launch_bounds__(256) void nk_combine4_kernel(const float4* __restrict__ din,
+                                                          const float4* __restrict__ dchild,
+                                                          const float4* __restrict__ G,
+                                                          const int32_t* __restrict__ iofs,
+                                                          const int32_t* __restrict__ ient,
+                                                          const int32_t* __restrict__ rowmap,
+                                                          int N, int L, int k,
+                                                          float4* __restrict__ dout) {
+  const int64_t total = (int64_t)N * L;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(t / L), m = (int)(t - (int64_t)n * L);
+    const int pc = rowmap[n];
+    const float4 a = din ? din[t] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4 b = dchild[t];
+    float4 v = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    if (pc >= 0 && G) {
+      float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      for (int e = iofs[m]; e < iofs[m + 1]; ++e) {
+        const float4 gv = G[(size_t)pc * L * k + ient[e]];
+        acc.x += gv.x;
+        acc.y += gv.y;
+        acc.z += gv.z;
+        acc.w += gv.w;
+      }
+      v.x += acc.x;
+      v.y += acc.y;
+      v.z += acc.z;
+      v.w += acc.w;
     }
     dout[t] = v;
   }
@@ -1114,10 +1201,19 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
   const double norm = (double)n_nonroot * (double)n_valid;
   const float scale = (float)((double)lambda_val / norm);
   const NkCe ce{seqs, v.cofs, v.cidx, seq_mask, scale, dlog, dchild, part};
-  if (!launch_logits(a, ns, st, logits, &ce))
-    hipLaunchKernelGGL(nk_ce_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
-                       seqs, logits, v.cofs, v.cidx, seq_mask, n_parents, L, Q, scale, dlog,
-                       dchild, part);
+  const char* v4e = std::getenv("TREX_NK_V4");  // "0": the generic kernels (A/B)
+  const bool v4 = Q == 4 && !(v4e && v4e[0] == '0');
+  if (!launch_logits(a, ns, st, logits, &ce)) {
+    if (v4)
+      hipLaunchKernelGGL(nk_ce4_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(seqs), reinterpret_cast<const float4*>(logits),
+                         v.cofs, v.cidx, seq_mask, n_parents, L, scale,
+                         reinterpret_cast<float4*>(dlog), reinterpret_cast<float4*>(dchild), part);
+    else
+      hipLaunchKernelGGL(nk_ce_kernel, dim3(grid1d((int64_t)n_parents * L, 256)), dim3(256), 0, st,
+                         seqs, logits, v.cofs, v.cidx, seq_mask, n_parents, L, Q, scale, dlog,
+                         dchild, part);
+  }
   if (int e = nk_err(fn)) return e;
   // few (parent, site) partials (the eval shape: 465): one block sums them
   // directly; otherwise two fixed levels (chunks, then the chunk sums)
@@ -1137,8 +1233,15 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
   // m (inverse CSR iofs / ient, ascending (site, j))
   if (k > 0) launch_logits_bwd(a, ns, st, dlog, G);
   (void)dpar;
-  hipLaunchKernelGGL(nk_combine_kernel, dim3(grid1d((int64_t)N * per, 256)), dim3(256), 0, st,
-                     d_seqs_in, dchild, k > 0 ? G : nullptr, v.iofs, v.ient, v.rowmap, N, L, Q, k,
-                     d_seqs);
+  if (v4)
+    hipLaunchKernelGGL(nk_combine4_kernel, dim3(grid1d((int64_t)N * L, 256)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(d_seqs_in),
+                       reinterpret_cast<const float4*>(dchild),
+                       k > 0 ? reinterpret_cast<const float4*>(G) : nullptr, v.iofs, v.ient,
+                       v.rowmap, N, L, k, reinterpret_cast<float4*>(d_seqs));
+  else
+    hipLaunchKernelGGL(nk_combine_kernel, dim3(grid1d((int64_t)N * per, 256)), dim3(256), 0, st,
+                       d_seqs_in, dchild, k > 0 ? G : nullptr, v.iofs, v.ient, v.rowmap, N, L, Q,
+                       k, d_seqs);
   return nk_err(fn);
 }
