@@ -55,6 +55,7 @@ extern "C" {
 
 const char* trex_last_error(void);
 /* ABI / plan-layout version.
+ * 10: trex_dp_root_total (run_sankoff for Q > 128 on the raw-table path).
  * 9: TREX_FLAG_SITE_REUSE and trex_site_flag_offset removed (flags other
  *    than TREX_FLAG_HARD_ROOT are refused).
  * 8: plan child descriptors may carry bit 28 and step words flag 8 (deferred
@@ -122,7 +123,9 @@ int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
  * Q up to 128 (leaf codes and ancestral states are int8): Q <= 64 on the
  * state-parallel / lane-per-site kernels, 64 < Q <= 128 on the large-alphabet
  * kernel (sankoff_bigq.hip, since ABI v7); Q > 128 returns
- * TREX_E_UNSUPPORTED.  Ragged batches take the same range.
+ * TREX_E_UNSUPPORTED (trex_amd.run_sankoff then takes the raw-table path:
+ * trex_run_dp, trex_backtrack_generic, trex_dp_root_total).  Ragged batches
+ * take the same range.
  * ---------------------------------------------------------------------- */
 int trex_sankoff_fwd(const int32_t* plan, int n_slots, const int8_t* leaves,
                      const float* cost, int B, int L, int n_all, int Q, float tau,
@@ -218,6 +221,14 @@ int trex_backtrack_generic(int root_node, const int32_t* root_state, const float
                            const float* bt, int n_all, int n_leaves, int L, int Q, int32_t* out,
                            void* stack_ws, int64_t stack_bytes, int64_t max_steps, int32_t* status,
                            void* stream);
+
+/* run_sankoff's total on a raw (L, n_all, Q) table (sankoff.py:187:
+ * dp[:, -1].min(axis=1).sum(), NaN propagating): per-site root minima into
+ * site_min fp32 [L] (scratch), their fp64 sum in a fixed order rounded to
+ * fp32 into *total.  run_sankoff's path for Q > 128 (the raw run_dp table,
+ * then this; trex_amd.run_sankoff), since ABI v10. */
+int trex_dp_root_total(const float* dp, int L, int n_all, int Q, float* site_min, float* total,
+                       void* stream);
 
 /* 1 when the DP / marginal tables for Q states are site-major
  * [B][n_int][L][Q], 0 when they are [B][n_int][Q][L].  Always 1 since

@@ -2,8 +2,10 @@
 vs the CPU oracle.
 
 trex sizes its tables from n_states with no cap (src/trex/sankoff.py:151-152);
-this build serves Q up to 128 (int8 leaf codes and ancestral states) and
-refuses larger alphabets with TREX_E_UNSUPPORTED.  Bars as everywhere: hard
+the engine serves Q up to 128 (int8 leaf codes and ancestral states) and
+refuses larger alphabets with TREX_E_UNSUPPORTED; run_sankoff then takes the
+raw-table kernels (trex_run_dp, trex_backtrack_generic, trex_dp_root_total),
+checked here bit-exact at Q = 129 and 257.  Bars as everywhere: hard
 DP table / totals / reconstruction bit-exact, hard gradient rtol 1e-6,
 softmin score and dC rtol 1e-5 elementwise, marginals by the per-entry
 fp32-D conditioning bound (tests/_cases.py).
@@ -125,3 +127,28 @@ def test_alphabet_above_128_is_refused(device):
         eng = SankoffEngine(TreePlan(ch), 10, 129, device)
         lv = torch.zeros((1, 4, 10), dtype=torch.int8, device=device)
         eng.forward(lv, torch.ones((129, 129), device=device), 0.0)
+
+
+@pytest.mark.parametrize("Q,L,n", [(129, 40, 12), (257, 9, 7)])
+def test_run_sankoff_past_the_engine_alphabet(device, Q, L, n):
+    """n_states > 128: run_sankoff on the raw-table kernels, bit-exact vs the
+    oracle (dp, reconstruction, total; sankoff.py:114-188), incl. a wrapped
+    negative and an out-of-range leaf state (the reference's dropped
+    scatter) and an odd n_leaves that disagrees with (n_all + 1) // 2."""
+    ch = random_topologies(1, n, seed=Q + L)[0]
+    adj = adjacency_from_children(ch)[0]
+    n_all = 2 * n - 1
+    rng = np.random.default_rng(Q * 3 + L)
+    seqs = rng.integers(0, Q, size=(n, L)).astype(np.float32)
+    seqs[0, 0] = -1.0  # wraps to Q - 1
+    seqs[1, 1] = Q + 3.0  # dropped: all-1e5 leaf row
+    cost = int_cost(Q, seed=Q)
+    for n_leaves in (n, n - 1):
+        recon, dp, total = run_sankoff(adj, cost, seqs, n_all, Q, n_leaves, return_path=True,
+                                       device=device)
+        r_recon, r_dp, r_total = run_sankoff_ref(adj, cost, seqs, n_all, Q, n_leaves,
+                                                 return_path=True)
+        np.testing.assert_array_equal(dp.cpu().numpy(), r_dp)
+        np.testing.assert_array_equal(recon.cpu().numpy(), r_recon)
+        assert float(total) == float(r_total)
+

@@ -277,7 +277,7 @@ def test_abi_version_matches_plan_layout():
     the stack depth (include/trex_hip.h); a binding that sized v5 plans
     itself must see the bump.  7 added the device step state (no plan
     change)."""
-    assert lib().trex_version() == 9
+    assert lib().trex_version() == 10
     ch = balanced_children(64, B=1)
     p = TreePlan(ch)
     assert p.n_slots == 5 and p.lane_slots == 12 and p.slot_word == 5 | (13 << 16)

@@ -56,6 +56,7 @@ SIGNATURES = {
     "trex_backtrack_workspace_bytes": (_c_i64, [_c_i, _c_i]),
     "trex_backtrack_generic": (_c_i, [_c_i, _p, _p, _p, _c_i, _c_i, _c_i, _c_i, _p, _p, _c_i64,
                                       _c_i64, _p, _p]),
+    "trex_dp_root_total": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _p, _p]),
     # tree-cost path
     "trex_tree_discretize": (_c_i, [_p, _c_i, _c_i, _c_i, _p, _p]),
     "trex_tree_update_seq": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _p, _p]),

@@ -211,6 +211,36 @@ __global__ __launch_bounds__(kRdThreads) void backtrack_generic_kernel(
   }
 }
 
+// run_sankoff's total over a raw table (sankoff.py:187: dp[:, -1].min(axis=1)
+// .sum(); jnp.min propagates NaN): per-site minimum of the root row, then one
+// workgroup sums the minima in fp64 in a fixed order (thread t: sites t,
+// t + 256, ...; then a fixed LDS tree) and rounds once to fp32
+__global__ __launch_bounds__(kRdThreads) void root_min_kernel(const float* __restrict__ dp, int L,
+                                                             int n_all, int Q,
+                                                             float* __restrict__ site_min) {
+  const int l = blockIdx.x * kRdThreads + threadIdx.x;
+  if (l >= L) return;
+  const float* d = dp + ((size_t)l * n_all + (n_all - 1)) * Q;
+  float m = d[0];
+  for (int j = 1; j < Q; ++j)
+    if (d[j] < m || is_nan(d[j])) m = d[j];
+  site_min[l] = m;
+}
+
+__global__ __launch_bounds__(kRdThreads) void root_total_kernel(const float* __restrict__ site_min,
+                                                               int L, float* __restrict__ total) {
+  __shared__ double part[kRdThreads];
+  double s = 0.0;
+  for (int l = threadIdx.x; l < L; l += kRdThreads) s += (double)site_min[l];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = kRdThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = (float)part[0];
+}
+
 int rd_check(const char* fn) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(TREX_E_HIP, "%s: %s", fn, hipGetErrorString(e));
@@ -266,5 +296,17 @@ extern "C" int trex_backtrack_generic(int root_node, const int32_t* root_state, 
   hipLaunchKernelGGL(backtrack_generic_kernel, dim3((L + kRdThreads - 1) / kRdThreads),
                      dim3(kRdThreads), 0, (hipStream_t)stream, root_node, root_state, dp, bt, n_all,
                      n_leaves, L, Q, static_cast<int2*>(stack_ws), out, max_steps, status);
+  return rd_check(fn);
+}
+
+extern "C" int trex_dp_root_total(const float* dp, int L, int n_all, int Q, float* site_min,
+                                  float* total, void* stream) {
+  const char* fn = "trex_dp_root_total";
+  if (n_all < 1 || L <= 0 || Q < 1 || !dp || !site_min || !total)
+    return set_error(TREX_E_ARG, "%s: bad arguments (n_all=%d L=%d Q=%d)", fn, n_all, L, Q);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(root_min_kernel, dim3((L + kRdThreads - 1) / kRdThreads), dim3(kRdThreads), 0,
+                     st, dp, L, n_all, Q, site_min);
+  hipLaunchKernelGGL(root_total_kernel, dim3(1), dim3(kRdThreads), 0, st, site_min, L, total);
   return rd_check(fn);
 }

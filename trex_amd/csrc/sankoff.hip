@@ -1455,7 +1455,7 @@ using namespace trex;
 
 extern "C" const char* trex_last_error(void) { return g_err; }
 
-extern "C" int trex_version(void) { return 9; }
+extern "C" int trex_version(void) { return 10; }
 
 extern "C" int trex_dp_site_major(int Q) {
   (void)Q;

@@ -302,14 +302,60 @@ def _prepare(adjacency_matrix, cost_matrix, sequences, n_all, n_states, n_leaves
     return plan, eng, codes, cost, seqs
 
 
+# the engine's alphabet limit (int8 leaf codes / ancestral states,
+# include/trex_hip.h); run_sankoff takes the raw-table kernels past it
+ENGINE_MAX_STATES = 128
+
+
+def _run_sankoff_raw(adjacency_matrix, cost_matrix, sequences, n_all, n_states, n_leaves,
+                     return_path, device):
+    """run_sankoff for n_states > ENGINE_MAX_STATES on the reference's own
+    tables (sankoff.py:141-188 step for step): the raw-table DP
+    (``trex_run_dp``: sentinel-filled (L, n_all, Q) table, (L, n_all, Q, 4)
+    backtracking table), the reference's DFS from the root row's first argmin
+    (``trex_backtrack_generic``), the total from ``trex_dp_root_total``."""
+    torch = _torch()
+    device = torch.device(device) if device is not None else _default_device()
+    adj = np.array(_to_host(adjacency_matrix), dtype=np.float32, copy=True)
+    if adj.shape != (n_all, n_all):
+        raise ValueError(f"adjacency_matrix must be ({n_all}, {n_all}), got {adj.shape}")
+    adj[-1, -1] = 0  # sankoff.py:141
+    seqs = _f32_dev(sequences, device)
+    if seqs.ndim != 2 or seqs.shape[0] < max(n_leaves, (n_all + 1) // 2):
+        raise ValueError(f"sequences must be (>= {max(n_leaves, (n_all + 1) // 2)}, L), "
+                         f"got {tuple(seqs.shape)}")
+    cost = _f32_dev(cost_matrix, device)
+    if tuple(cost.shape) != (n_states, n_states):
+        raise ValueError(f"cost_matrix must be ({n_states}, {n_states})")
+    L = int(seqs.shape[1])
+    dp, bt = vectorized_dp(adj, torch.full((L, n_all, n_states), SENTINEL, dtype=torch.float32,
+                                           device=device),
+                           torch.zeros((L, n_all, n_states, 4), dtype=torch.float32,
+                                       device=device), seqs, cost, device=device)
+    recon = torch.zeros((n_all, L), dtype=torch.float32, device=device)
+    recon[:n_leaves] = seqs[:n_leaves]
+    if return_path:
+        chars = vmapped_backtrack(n_all - 1, None, bt, n_all, n_leaves, dp=dp, device=device)
+        recon[n_leaves:] = chars[n_leaves:].to(torch.float32)
+    site_min = torch.empty(L, dtype=torch.float32, device=device)
+    total = torch.empty((), dtype=torch.float32, device=device)
+    check(lib().trex_dp_root_total(ptr(dp), L, n_all, n_states, ptr(site_min), ptr(total),
+                                   stream_handle(device)))
+    return recon, dp, total
+
+
 def run_sankoff(adjacency_matrix, cost_matrix, sequences, n_all: int, n_states: int,
                 n_leaves: int, *, return_path: bool = False, device=None):
     """Sankoff over one tree (sankoff.py:114-188).
 
     Returns (reconstructed (n_all, L) f32, dp (L, n_all, Q) f32, total f32[]) as
-    device tensors with trex's layouts and values.
+    device tensors with trex's layouts and values.  Alphabets past the
+    engine's 128 states run on the raw-table kernels (``_run_sankoff_raw``).
     """
     torch = _torch()
+    if n_states > ENGINE_MAX_STATES:
+        return _run_sankoff_raw(adjacency_matrix, cost_matrix, sequences, n_all, n_states,
+                                n_leaves, return_path, device)
     plan, eng, codes, cost, seqs = _prepare(adjacency_matrix, cost_matrix, sequences, n_all,
                                             n_states, n_leaves, device)
     f = eng.forward(codes, cost, 0.0, dp=True)
