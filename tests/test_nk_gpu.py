@@ -317,12 +317,15 @@ def test_register_kernels_bitwise_the_rolled_kernels(device, monkeypatch, Q, k):
     np.testing.assert_allclose(got, ref, rtol=RTOL, atol=1e-6)
 
 
-@pytest.mark.parametrize("k,mask", [(1, False), (2, True), (4, True)])
-def test_q4_vector_kernels_bitwise_the_generic_kernels(device, monkeypatch, k, mask):
-    """Q = 4's float4 cross-entropy / combine kernels (csrc/nk.hip nk_ce4_kernel,
-    nk_combine4_kernel) == the generic per-state kernels (TREX_NK_V4=0) bit for
-    bit: loss and d ancestors, with and without the site mask."""
-    c = _case(64, 300, 4, k, seed=40 + k, mask=mask)
+@pytest.mark.parametrize("k,mask,L", [(1, False, 300), (2, True, 300), (4, True, 300),
+                                      (4, True, 3000)])
+def test_q4_vector_kernels_bitwise_the_generic_kernels(device, monkeypatch, k, mask, L):
+    """Q = 4's float4 cross-entropy / combine kernels (csrc/nk.hip nk_ce4_kernel;
+    nk_combine4_lds_kernel when a parent's G block fits the LDS, L = 300,
+    else nk_combine4_kernel, L = 3000 at k = 4) == the generic per-state
+    kernels (TREX_NK_V4=0) bit for bit: loss and d ancestors, with and
+    without the site mask."""
+    c = _case(64, L, 4, k, seed=40 + k, mask=mask)
     land = NK.NKLandscape(c["inter"], c["F"], 4, device)
     a = torch.as_tensor(c["anc"], device=device)
     s = torch.as_tensor(c["S0"], device=device)

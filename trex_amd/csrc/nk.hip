@@ -942,6 +942,49 @@ __global__ __launch_bounds__(256) void nk_combine4_kernel(const float4* __restri
   }
 }
 
+// Q = 4, one workgroup per node row n when the parent row's per-slot
+// gradients G [L][k] (16 B each) fit the LDS: the block is staged with
+// coalesced 16-B loads and the inverse-CSR gathers read LDS (each 16-B
+// gather from L2 pulled a whole 128-B line: 8x the bytes, 40 us at the DNA
+// shape); sums in nk_combine4_kernel's order (bitwise the same)
+constexpr int kNkCombineThreads = 1024;
+constexpr int64_t kNkCombineLds = 160 * 1024;
+__global__ __launch_bounds__(kNkCombineThreads) void nk_combine4_lds_kernel(
+    const float4* __restrict__ din, const float4* __restrict__ dchild,
+    const float4* __restrict__ G, const int32_t* __restrict__ iofs,
+    const int32_t* __restrict__ ient, const int32_t* __restrict__ rowmap, int L, int k,
+    float4* __restrict__ dout) {
+  extern __shared__ __attribute__((aligned(16))) float4 gl[];
+  const int n = blockIdx.x;
+  const int pc = rowmap[n];
+  const size_t rb = (size_t)n * L;
+  if (pc >= 0) {  // block-uniform
+    const float4* gp = G + (size_t)pc * L * k;
+    for (int e = threadIdx.x; e < L * k; e += kNkCombineThreads) gl[e] = gp[e];
+    __syncthreads();
+  }
+  for (int m = threadIdx.x; m < L; m += kNkCombineThreads) {
+    const float4 a = din ? din[rb + m] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4 b = dchild[rb + m];
+    float4 v = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    if (pc >= 0) {
+      float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      for (int e = iofs[m]; e < iofs[m + 1]; ++e) {
+        const float4 gv = gl[ient[e]];
+        acc.x += gv.x;
+        acc.y += gv.y;
+        acc.z += gv.z;
+        acc.w += gv.w;
+      }
+      v.x += acc.x;
+      v.y += acc.y;
+      v.z += acc.z;
+      v.w += acc.w;
+    }
+    dout[rb + m] = v;
+  }
+}
+
 int64_t ipow(int b, int e) {
   int64_t r = 1;
   for (int i = 0; i < e; ++i) r *= b;
@@ -1233,7 +1276,19 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
   // m (inverse CSR iofs / ient, ascending (site, j))
   if (k > 0) launch_logits_bwd(a, ns, st, dlog, G);
   (void)dpar;
-  if (v4)
+  const int64_t glds = (int64_t)L * k * 16;
+  if (v4 && k > 0 && glds <= kNkCombineLds) {
+    static const bool attr = [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(nk_combine4_lds_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNkCombineLds);
+      return true;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(nk_combine4_lds_kernel, dim3(N), dim3(kNkCombineThreads), (size_t)glds, st,
+                       reinterpret_cast<const float4*>(d_seqs_in),
+                       reinterpret_cast<const float4*>(dchild), reinterpret_cast<const float4*>(G),
+                       v.iofs, v.ient, v.rowmap, L, k, reinterpret_cast<float4*>(d_seqs));
+  } else if (v4)
     hipLaunchKernelGGL(nk_combine4_kernel, dim3(grid1d((int64_t)N * L, 256)), dim3(256), 0, st,
                        reinterpret_cast<const float4*>(d_seqs_in),
                        reinterpret_cast<const float4*>(dchild),
