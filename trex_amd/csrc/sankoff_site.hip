@@ -354,6 +354,11 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
       load_row_direct(rr, row, v);
   };
   auto load_row = [&](int row, float (&v)[kSQ]) { load_row_r(rdp, row, v); };
+#ifdef SITE_DIAG_HOTROW  // diagnostic: the adjoint's row loads all read row 0 (cache-hot; wrong math)
+#define SITE_ADJ_ROW(x) 0
+#else
+#define SITE_ADJ_ROW(x) (x)
+#endif
   auto slot_get = [&](int sl, float (&v)[kSQ]) {
 #pragma unroll
     for (int j = 0; j < kSQ; ++j) v[j] = slots[(size_t)sl * kSlotF + j * kWave + lane];
@@ -868,9 +873,9 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
             if (ie.w > 1 && keep_s) {
               // the forward's D and s rows of this child (no mat-vec)
               float sv[kSQ], md, u[kSQ];
-              load_row(ie.x, d);
+              load_row(SITE_ADJ_ROW(ie.x), d);
               weights_u(d, md, u);
-              load_row_r(rsr, ie.x, sv);
+              load_row_r(rsr, SITE_ADJ_ROW(ie.x), sv);
               // lanes past L read 0 (their g is 0): keep r = g / s finite
 #pragma unroll
               for (int i = 0; i < kSQ; ++i) sv[i] = active ? sv[i] : 1.0f;
