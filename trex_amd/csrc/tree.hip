@@ -551,24 +551,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto compute = [&](const unsigned char* buf) {
     int a = a0, b = b0, ap = -1;
     h8 ah, al;
+    // B fragments one tile ahead: tile t + 1's reads are issued before tile
+    // t's MFMAs (the A fragment only when the row strip changes: a wave's
+    // 13 tiles span 2-3 strips; LDS read bytes per chunk 416 -> ~240 KB per CU)
+    h8 bh = *reinterpret_cast<const h8*>(buf + b * (32 * kG3Stride) + lofs);
+    h8 bl = *reinterpret_cast<const h8*>(buf + b * (32 * kG3Stride) + lofs + 32);
 #pragma unroll
     for (int t = 0; t < kG3Tiles; ++t) {
-      // the A fragment only when the row strip changes (a wave's 13 tiles
-      // span 2-3 strips): LDS read bytes per chunk 416 -> ~240 KB per CU
       if (a != ap) {
         const unsigned char* pa = buf + a * (32 * kG3Stride) + lofs;
         ah = *reinterpret_cast<const h8*>(pa);
         al = *reinterpret_cast<const h8*>(pa + 32);
         ap = a;
       }
-      const unsigned char* pb = buf + b * (32 * kG3Stride) + lofs;
-      const h8 bh = *reinterpret_cast<const h8*>(pb);
-      const h8 bl = *reinterpret_cast<const h8*>(pb + 32);
-      acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
-      if (++b >= ns) {
-        a = min(a + 1, ns - 1);
-        b = a > t0s ? a : t0s;
+      const bool wrap = b + 1 >= ns;
+      const int an = wrap ? min(a + 1, ns - 1) : a;
+      const int bn = wrap ? (an > t0s ? an : t0s) : b + 1;
+      h8 bhn = bh, bln = bl;
+      if (t + 1 < kG3Tiles) {
+        const unsigned char* pb = buf + bn * (32 * kG3Stride) + lofs;
+        bhn = *reinterpret_cast<const h8*>(pb);
+        bln = *reinterpret_cast<const h8*>(pb + 32);
       }
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch reads above the MFMAs
+      acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
+      bh = bhn;
+      bl = bln;
+      a = an;
+      b = bn;
     }
   };
 
