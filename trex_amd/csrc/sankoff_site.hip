@@ -54,6 +54,40 @@ constexpr int kTabF = (kSQ + 1) * kSQ + kSQ;  // leaf messages T[Q + 1][kSQ] + 1
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+#ifndef SITE_DC_BF16
+#define SITE_DC_BF16 1  // 0: the dC outer products on f32 32x32x2 MFMAs (A/B, PERFLOG)
+#endif
+
+// eight floats (two float4 at p0, p1) split exactly into truncated bf16
+// pieces x = h + m + l, packed two per dword in k order
+__device__ __forceinline__ void split3(const float* p0, const float* p1, u32x4& h, u32x4& m, u32x4& l) {
+  const float4 a = *reinterpret_cast<const float4*>(p0), b = *reinterpret_cast<const float4*>(p1);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t hb[2], mb[2], lb[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float x = v[2 * q + e];
+      const float xh = __uint_as_float(__float_as_uint(x) & 0xFFFF0000u);
+      const float r1 = x - xh;
+      const float xm = __uint_as_float(__float_as_uint(r1) & 0xFFFF0000u);
+      hb[e] = __float_as_uint(xh);
+      mb[e] = __float_as_uint(xm);
+      lb[e] = __float_as_uint(r1 - xm);
+    }
+    // high halves of (e0, e1) -> one dword, e0 in the low half
+    h[q] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
+    m[q] = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
+    l[q] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+  }
+}
+
+__device__ __forceinline__ f16v mfma_bf(const u32x4& a, const u32x4& b, const f16v& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+
 struct SiteArgs {
   const int* lanes;  // lane programs (trex_common.h)
   int64_t stride;    // ints per tree region
@@ -636,6 +670,26 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
       wave_sync();
       return;
 #endif
+#if SITE_DC_BF16
+      // r and u split exactly into three truncated 8-bit pieces each (hi + mid
+      // + lo); the six products down to 2^-16 of |r u| (hl, lh, mm, mh, hm, hh,
+      // smallest first) on v_mfma_f32_32x32x16_bf16, k = 16 sites: dropped
+      // terms < 2^-23 |r u| per product (r, u >= 0: no cancellation), 24 MFMAs
+      // of 32 cycles per 64 sites instead of 32 f32 MFMAs of 64
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int sg = 16 * t + 8 * khalf;  // this lane's 8 sites of the k-step
+        u32x4 ah, am, al, bh, bm, bl;
+        split3(xr + swz(rrow, sg), xr + swz(rrow, sg + 4), ah, am, al);
+        split3(xu + swz(rrow, sg), xu + swz(rrow, sg + 4), bh, bm, bl);
+        acc1 = mfma_bf(ah, bl, acc1);
+        acc1 = mfma_bf(al, bh, acc1);
+        acc1 = mfma_bf(am, bm, acc1);
+        acc1 = mfma_bf(am, bh, acc1);
+        acc1 = mfma_bf(ah, bm, acc1);
+        acc1 = mfma_bf(ah, bh, acc1);
+      }
+#else
 #pragma unroll
       for (int t4 = 0; t4 < 8; ++t4) {
         const int sg = khalf * 32 + 4 * t4;
@@ -646,6 +700,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(ra.z, ub.z, acc1, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(ra.w, ub.w, acc1, 0, 0, 0);
       }
+#endif
       wave_sync();
     };
     auto outer = [&](const float (&r)[kSQ], const float (&u)[kSQ]) {
