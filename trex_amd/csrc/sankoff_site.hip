@@ -65,21 +65,17 @@ __device__ __forceinline__ void split3(const float* p0, const float* p1, u32x4& 
   const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    uint32_t hb[2], mb[2], lb[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const float x = v[2 * q + e];
-      const float xh = __uint_as_float(__float_as_uint(x) & 0xFFFF0000u);
-      const float r1 = x - xh;
-      const float xm = __uint_as_float(__float_as_uint(r1) & 0xFFFF0000u);
-      hb[e] = __float_as_uint(xh);
-      mb[e] = __float_as_uint(xm);
-      lb[e] = __float_as_uint(r1 - xm);
-    }
+    // the two residual subtractions of a pair as one v_pk_add_f32 each
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    const f2 x = pk(v[2 * q], v[2 * q + 1]);
+    const u2 xb = __builtin_bit_cast(u2, x);
+    const f2 r1 = x - __builtin_bit_cast(f2, xb & 0xFFFF0000u);
+    const u2 mb = __builtin_bit_cast(u2, r1) & 0xFFFF0000u;
+    const u2 lb = __builtin_bit_cast(u2, r1 - __builtin_bit_cast(f2, mb));
     // high halves of (e0, e1) -> one dword, e0 in the low half
-    h[q] = __builtin_amdgcn_perm(hb[1], hb[0], 0x07060302u);
-    m[q] = __builtin_amdgcn_perm(mb[1], mb[0], 0x07060302u);
-    l[q] = __builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u);
+    h[q] = __builtin_amdgcn_perm(xb.y, xb.x, 0x07060302u);
+    m[q] = __builtin_amdgcn_perm(mb.y, mb.x, 0x07060302u);
+    l[q] = __builtin_amdgcn_perm(lb.y, lb.x, 0x07060302u);
   }
 }
 
@@ -712,7 +708,6 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
       wave_sync();
       outer_mfma();
     };
-    // acc2 += g (sum of the leaf children's one-hot rows)^T; nleaf leaf descs
     // acc2 += g (sum of the leaf children's one-hot rows)^T on the bf16 matrix
     // core: g split exactly into three 8-bit pieces (hi + mid + lo, truncated,
     // residual < 2^-23 |g|) against exact 0 / 1 / 2 one-hot counts, k = 16
@@ -731,28 +726,8 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int sg = 16 * t + 8 * khalf;  // this lane's 8 sites of the k-step
-        const float4 ga = *reinterpret_cast<const float4*>(xr + swz(rrow, sg));
-        const float4 gb = *reinterpret_cast<const float4*>(xr + swz(rrow, sg + 4));
-        const float gv[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
         u32x4 ph, pm, pl, pb;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t h2[2], m2[2], l2[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const float x = gv[2 * q + e];
-            const float xh = __uint_as_float(__float_as_uint(x) & 0xFFFF0000u);
-            const float r1 = x - xh;
-            const float xm = __uint_as_float(__float_as_uint(r1) & 0xFFFF0000u);
-            const float xl = r1 - xm;
-            h2[e] = __float_as_uint(xh) >> 16;
-            m2[e] = __float_as_uint(xm) >> 16;
-            l2[e] = __float_as_uint(xl) >> 16;
-          }
-          ph[q] = h2[0] | (h2[1] << 16);
-          pm[q] = m2[0] | (m2[1] << 16);
-          pl[q] = l2[0] | (l2[1] << 16);
-        }
+        split3(xr + swz(rrow, sg), xr + swz(rrow, sg + 4), ph, pm, pl);
         const uint32_t w0[2] = {l0 ? c0[sg >> 2] : 0xFFFFFFFFu, l0 ? c0[(sg >> 2) + 1] : 0xFFFFFFFFu};
         const uint32_t w1[2] = {l1 ? c1[sg >> 2] : 0xFFFFFFFFu, l1 ? c1[(sg >> 2) + 1] : 0xFFFFFFFFu};
 #pragma unroll
