@@ -521,8 +521,12 @@ struct KArgs {
 // 0, W[code][i][j] = its adjoint weight (divided by K_ij in the factored
 // form) at kWTab -- both depend on the code only, so every leaf / sentinel
 // child is a table lookup in both sweeps; then the slot stack
-// [n_slots + 1][64][Q*SPT] (slot n_slots = root cotangent), then the leaf
-// tile [nl][64*SPT] i8 (raw codes, normalised to [0, Q] at use).
+// [max(n_slots, 1)][64][Q*SPT], then the leaf tile [nl][64*SPT] i8 (raw
+// codes, normalised to [0, Q] at use).  The root's cotangent goes to slot 0:
+// it is written after the forward has consumed every slot and read by the
+// first reverse step (always the root's), before any child cotangent is
+// written, and slots are lane-private (a dedicated root slot cost 1 KiB per
+// wave: 24 -> 29 waves per CU at C4's 3 slots).
 constexpr int kTabFloats = 128;
 constexpr int kWTab = 32;  // (Q + 1) Q <= 20 message floats precede the weights
 #ifndef TREX_ADJ_RING
@@ -575,8 +579,8 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 
   float* tab = lds;
   float* slots = lds + kTabFloats;
-  const int kRootSlot = A.n_slots;
-  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)(A.n_slots + 1) * Q * kWave * SPT);
+  constexpr int kRootSlot = 0;
+  int8_t* lleaf = reinterpret_cast<int8_t*>(slots + (size_t)max(A.n_slots, 1) * Q * kWave * SPT);
 
   // ---- once per wave: the leaf tables.  Lane c <= Q builds row c from the
   // child row D = (0 at c, 1e5 elsewhere; all 1e5 for c = Q).  When the 1e5
@@ -1175,7 +1179,7 @@ int check_shape(const char* fn, int B, int L, int n_all, int Q, Shape* sh) {
 int tiles_for(int L, int spt) { return (L + kWave * spt - 1) / (kWave * spt); }
 
 size_t lds_bytes(int n_slots, int nl, int Q, int spt) {
-  const size_t b = (size_t)kTabFloats * 4 + (size_t)(n_slots + 1) * Q * kWave * spt * 4 +
+  const size_t b = (size_t)kTabFloats * 4 + (size_t)std::max(n_slots, 1) * Q * kWave * spt * 4 +
                    (size_t)nl * kWave * spt;
   return (b + 15) & ~(size_t)15;
 }
