@@ -511,11 +511,18 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=25
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
+    red0 = (opt.reducer.calls, opt.reducer.bytes) if opt.reducer is not None else (0, 0)
     t0 = time.perf_counter()
     for k in range(steps):
         loss = opt.step(temp(warmup + k), noise[k % 4], next_temperature=temp(warmup + k + 1))
     torch.cuda.synchronize()
     sec = (time.perf_counter() - t0) / steps
+    gram_ar = None
+    if opt.reducer is not None:
+        # the Gram exchange of one timed step (GramReducer's own count)
+        gram_ar = {"calls_per_step": (opt.reducer.calls - red0[0]) / steps,
+                   "bytes_per_step": (opt.reducer.bytes - red0[1]) // steps,
+                   "ranks": dist.get_world_size(group)}
     if dist_on:
         t = torch.tensor([sec], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -538,6 +545,7 @@ def c5_line(torch, device, steps=20, warmup=3, rank=0, world=1, gemm="x3", nl=25
            "taxa": nl, "sites": L, "sites_rank0": hi - lo if rank == 0 else None,
            "scaling": "strong" if dist_on else None, "loss_last": float(loss),
            "gemm": opt.gemm, "leaf_codes": opt.codes is not None,
+           "gram_allreduce": gram_ar,
            "roofline": {"bound": "hbm", "algorithmic_bytes_per_step": step_bytes,
                         "achieved": round(step_bytes / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(step_bytes / sec / 1e9 / HBM_PEAK_GBS, 4)}}
@@ -684,6 +692,15 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=device)
+        # the group really spans N ranks: an all-reduce of ones on it (with
+        # RCCL, on the device) must come back as N, the launcher's WORLD_SIZE
+        ones = torch.ones(1, dtype=torch.float32, device=device)
+        dist.all_reduce(ones)
+        torch.cuda.synchronize()
+        rccl_ranks = int(round(float(ones.item())))
+        if rccl_ranks != world or dist.get_world_size() != world:
+            raise SystemExit(f"process group spans {rccl_ranks} ranks (get_world_size "
+                             f"{dist.get_world_size()}), WORLD_SIZE says {world}")
 
     from trex_amd import SankoffEngine
     from trex_amd.distributed import shard_bounds
@@ -713,6 +730,9 @@ def main():
     reds = [red, torch.zeros_like(red)]
     done = [torch.cuda.Event(), torch.cuda.Event()]
     it = [0]
+    # timed steps' all-reduces: HIP events on the comm stream around each one
+    ar_events = []
+    ar_timing = [False]
 
     def run_once():
         if graph is not None:
@@ -729,7 +749,13 @@ def main():
             buf[Q * Q:].copy_(step.out_f["tree_score"].sum().view(1))
             comm.wait_stream(cur)
             with torch.cuda.stream(comm):
+                if ar_timing[0]:
+                    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev[0].record(comm)
                 dist.all_reduce(buf)
+                if ar_timing[0]:
+                    ev[1].record(comm)
+                    ar_events.append(ev)
                 done[i].record(comm)
 
     for _ in range(args.warmup):
@@ -738,6 +764,7 @@ def main():
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
+    ar_timing[0] = dist_on
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run_once()
@@ -745,10 +772,23 @@ def main():
     if dist_on:
         dist.barrier()
     el = time.perf_counter() - t0
+    ar_timing[0] = False
+    dist_info = None
     if dist_on:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
+        # every rank's own time (all_gather), then the MAX the line reports
+        mine = torch.tensor([el], dtype=torch.float64, device=device)
+        per_rank = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(per_rank, mine)
+        t = mine.clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+        ar_us = [a.elapsed_time(b) * 1e3 for a, b in ar_events]
+        dist_info = {"rccl_ranks": rccl_ranks, "world_size": dist.get_world_size(),
+                     "ms_per_step_per_rank": [round(float(x.item()) / args.steps * 1e3, 4)
+                                              for x in per_rank],
+                     "allreduce_bytes": red.numel() * red.element_size(),
+                     "allreduce_us_mean_rank0": round(sum(ar_us) / max(len(ar_us), 1), 2),
+                     "allreduce_count": len(ar_us)}
 
     n_int = n - 1
     units = args.trees * L * n_int * Q  # the whole batch, all ranks
@@ -819,9 +859,13 @@ def main():
                                   "the next step" if dist_on else ""),
                    "trees": args.trees, "trees_rank0": B, "taxa": n, "sites": L, "states": Q,
                    "tau": tau, "hipgraph": use_graph, "parallelism": f"tree-batch x{world}",
-                   "process_group": dist.get_backend() if dist_on else None},
+                   "process_group": dist.get_backend() if dist_on else None,
+                   "rccl_ranks": dist_info["rccl_ranks"] if dist_info else None,
+                   "world_size": dist_info["world_size"] if dist_info else None},
         "roofline": roofline,
     }
+    if dist_info:
+        result["dist"] = dist_info
     if rank == 0 and not dist_on:
         hinfo, threads = host_cpu()
         threads = args.cpu_threads or threads

@@ -100,10 +100,15 @@ int64_t trex_plan_ints(int B, int n_all);
 int trex_plan_build(const int32_t* children, int B, int n_all, int32_t* plan,
                     int32_t* info);
 
-/* Workspace (device bytes) needed by fwd/bwd for a given shape.  It holds
- * per-block partial sums and arrival counters for the in-kernel,
- * fixed-order (bitwise reproducible) reductions; zero it once with
- * trex_workspace_init before first use (the kernels leave it zeroed). */
+/* Workspace (device bytes) fwd/bwd/fwd_bwd use for a given shape: the
+ * per-work-item fp64 partials (tree score, Q*Q dC) that a fixed-order reduce
+ * kernel sums (bitwise reproducible), and for 4 < Q <= 64 the lane-per-site
+ * kernel's gate words, K / K^T and cherry tables.  For 4 < Q <= 20 the value
+ * also covers a region the size of the DP table (B * n_int * L * Q * 4 bytes)
+ * where the fused call keeps its forward's softmin row sums for its adjoint;
+ * a smaller workspace (down to the size without that region) is accepted
+ * and the fused kernel then recomputes those sums.  Zero it once with
+ * trex_workspace_init before first use. */
 int64_t trex_workspace_bytes(int B, int L, int n_all, int Q);
 int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);
 

@@ -136,6 +136,14 @@ def test_bench_rccl_one_rank_rehearsal(tmp_path):
     assert len(lines) == 1, r.stdout[-2000:]
     res = json.loads(lines[0])
     assert res["n_gpus"] == 1 and res["config"]["process_group"] == "nccl"
+    # the self-verifying fields of the driver's N-GPU line
+    assert res["config"]["rccl_ranks"] == 1 and res["config"]["world_size"] == 1
+    d = res["dist"]
+    assert d["rccl_ranks"] == 1 and len(d["ms_per_step_per_rank"]) == 1
+    assert d["allreduce_count"] == steps and d["allreduce_us_mean_rank0"] > 0
+    assert d["allreduce_bytes"] == (states * states + 1) * 4
+    ga = res["c5"]["gram_allreduce"]
+    assert ga["ranks"] == 1 and ga["calls_per_step"] == 1 and ga["bytes_per_step"] > 0
     assert "RCCL all-reduce" in res["config"]["workload"]
     assert res["c5"]["scaling"] == "strong" and res["c5"]["n_gpus"] == 1
 

@@ -31,7 +31,8 @@ import numpy as np
 import pytest
 import torch
 
-from _cases import (assert_bound_close, assert_dp_close, assert_grad_close, hamming, random_leaves,
+from _cases import (EPS_VJP, assert_bound_close, assert_dp_close, assert_grad_close, hamming,
+                    random_leaves, softmax_vjp_bound, tree_param_select,
                     random_topologies, simulate_leaves, surrogate_grad_bounds)
 from oracle import cpu_port
 from oracle import tree_ref as T
@@ -201,6 +202,7 @@ def test_c5_full_size_steps_vs_fp64(device, gemm):
     nz = _dev(noise, device)
     temps = [2.0, 1.9996, 1.9992]
     losses = []
+    ratios = {k: [] for k in ("dA", "dS", "d tree_params", "ancestors", "ancestors at cap")}
     for k in range(3):
         T_k = temps[k]
         nxt = temps[k + 1] if k + 1 < len(temps) else T_k
@@ -222,38 +224,50 @@ def test_c5_full_size_steps_vs_fp64(device, gemm):
         del F
         cg = T_k * T.enforce_graph_constraints_grad(A64, 10.0)
         bS, bA = surrogate_grad_bounds(S64, A64, SOFT_RTOL, constraint_grad=cg)
-        assert_bound_close(opt.dA.cpu().numpy(), dA64, bA, what="dA")
-        assert_bound_close(opt.dS[nl:].cpu().numpy(), dS64[nl:], bS[nl:], what="dS")
-        del bS, bA
-        # d tree_params = A (dA - sum_k A dA) per row (softmax VJP, tree.py:50-107):
-        # dA ~ (E_i + E_j)/2 - G_ij ~ 5e4 here, so dA's own fp32 rounding (which
-        # the reference's fp32 autodiff has too) reaches d tree_params as
-        # ~eps32 * A_ij * max_k |dA_ik| -- the conditioning bound, written out:
+        ratios["dA"].append(assert_bound_close(opt.dA.cpu().numpy(), dA64, bA, what="dA"))
+        ratios["dS"].append(assert_bound_close(opt.dS[nl:].cpu().numpy(), dS64[nl:], bS[nl:],
+                                               what="dS"))
+        # d tree_params = A (dA - sum_k A dA) per row (update_tree's softmax
+        # VJP, tree.py:50-107), per entry: the dA bound just asserted carried
+        # through that VJP, plus the VJP's own fp32 rounding at the exact
+        # cotangent's magnitude (tests/_cases.py loss_grad_bounds)
         g_th = _f64(opt.grads["tree_params"])
         ref_th = T.update_tree_vjp(p64["tree_params"], noise, 1.0, None, A64, dA64)
-        cond = 16 * 1.2e-7 * A64[:-1, nl:] * np.abs(dA64[:-1]).max(axis=1, keepdims=True)
-        err = np.abs(g_th - ref_th)
-        assert np.all(err <= SOFT_RTOL * np.abs(ref_th).max()
-                      + np.maximum(SOFT_RTOL * np.abs(ref_th), cond)), err.max()
+        dz = (softmax_vjp_bound(A64, bA, axis=1)
+              + EPS_VJP * softmax_vjp_bound(A64, np.abs(dA64), axis=1))
+        ratios["d tree_params"].append(assert_bound_close(
+            g_th, ref_th, tree_param_select(dz, ref_th.shape[1]), what="d tree_params"))
+        del bA, dz
         # tree_params: fp64 Adam of the GPU's own gradient, to fp32 rounding
         new_th = _f64(opt.params["tree_params"])
         want = _adam64(p64["tree_params"], g_th, mu0["tree_params"], nu0["tree_params"],
                        k + 1, lr)
         slack = 4.8e-7 * np.abs(want) + 1e-5 * lr
         assert np.all(np.abs(new_th - want) <= slack), np.abs(new_th - want).max()
-        # ancestors: fused VJP + Adam vs fp64, error propagated from dS's bar
+        # ancestors: fused VJP + Adam vs fp64.  The gradient's bound per entry
+        # is the asserted dS bound through update_seq's softmax VJP plus the
+        # VJP's own rounding (loss_grad_bounds), then _adam_tol carries it
+        # through one Adam update from the GPU's own state
         anc = p64["ancestors"]
         S_anc = S64[nl:]
         g_anc = T.update_seq_vjp(anc, T_k, S_anc, dS64[nl:])
-        e_dS = SOFT_RTOL * np.abs(dS64[nl:]).max()
-        # |d g| <= T S (|d dS| + sum_q S |d dS|) + fp32 rounding of the VJP
-        b = T_k * S_anc * (2 * e_dS + 8 * 1.2e-7 * np.abs(dS64[nl:]).max(axis=-1, keepdims=True))
-        del S64, dS64
+        b = T_k * (softmax_vjp_bound(S_anc, bS[nl:])
+                   + EPS_VJP * softmax_vjp_bound(S_anc, np.abs(dS64[nl:])))
+        del S64, dS64, bS
         tol, cap = _adam_tol(g_anc, b, mu0["ancestors"], nu0["ancestors"], k + 1, lr)
         want = _adam64(anc, g_anc, mu0["ancestors"], nu0["ancestors"], k + 1, lr)
         new_anc = _f64(opt.params["ancestors"])
-        err = np.abs(new_anc - want)
-        assert np.all(err <= tol + 4.8e-7 * np.abs(want) + 1e-5 * lr), (err - tol).max()
-        assert np.mean(tol >= cap) < 1e-2
-        del anc, S_anc, g_anc, b, tol, want, new_anc, err
+        # + the update's own fp32 rounding (a few ulps of the parameter and of
+        # the lr-sized step)
+        ratios["ancestors"].append(assert_bound_close(
+            new_anc, want, tol + 4.8e-7 * np.abs(want) + 4.8e-7 * lr * 2, what="ancestors"))
+        # entries whose gradient bound straddles 0 may move by the sign-flip
+        # cap (Adam's first steps are ~lr sign(g)); that is a property of the
+        # data, measured here, and the check is only meaningful if it is rare
+        at_cap = float(np.mean(tol >= cap))
+        ratios["ancestors at cap"].append(at_cap)
+        assert at_cap < 1e-2, at_cap
+        del anc, S_anc, g_anc, b, tol, want, new_anc
+    print(f"C5 {gemm}: max err / bound per step", {k: [f"{x:.3g}" for x in v]
+                                                   for k, v in ratios.items()})
     assert losses[0] > losses[1] > losses[2]

@@ -949,6 +949,7 @@ __global__ __launch_bounds__(256) void nk_combine4_kernel(const float4* __restri
 // shape); sums in nk_combine4_kernel's order (bitwise the same)
 constexpr int kNkCombineThreads = 1024;
 constexpr int64_t kNkCombineLds = 160 * 1024;
+inline bool misaligned16(const void* p) { return p && (reinterpret_cast<uintptr_t>(p) & 15u); }
 __global__ __launch_bounds__(kNkCombineThreads) void nk_combine4_lds_kernel(
     const float4* __restrict__ din, const float4* __restrict__ dchild,
     const float4* __restrict__ G, const int32_t* __restrict__ iofs,
@@ -1199,6 +1200,9 @@ extern "C" int trex_nk_parental_logits(const float* seqs, const int32_t* rows, i
   if (int e = nk_check(fn, L, Q, k)) return e;
   if (!seqs || !rows || R <= 0 || !fitness || !logits || (k > 0 && !interactions))
     return set_error(TREX_E_ARG, "%s: null pointer / bad R", fn);
+  if (Q == 4 && (misaligned16(seqs) || misaligned16(logits)))
+    return set_error(TREX_E_ARG, "%s: Q = 4 rows are read as float4: pointers must be 16-byte "
+                     "aligned", fn);
   NkArgs a{seqs, rows, interactions, fitness, R, L, Q, k, (int)ipow(Q, k)};
   const int ns = nk_slices(R, L, Q, k);
   launch_logits(a, ns, (hipStream_t)stream, logits);
@@ -1219,6 +1223,10 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
     return set_error(TREX_E_ARG, "%s: null pointer / bad sizes", fn);
   if (workspace_bytes < trex_nk_workspace_bytes(N, L, Q, k, n_parents))
     return set_error(TREX_E_ARG, "%s: workspace too small", fn);
+  if (Q == 4 && (misaligned16(seqs) || misaligned16(d_seqs) || misaligned16(d_seqs_in) ||
+                 misaligned16(workspace)))
+    return set_error(TREX_E_ARG, "%s: Q = 4 rows are read as float4: pointers must be 16-byte "
+                     "aligned", fn);
   if (!pos_finite_f32(n_valid) || n_nonroot <= 0)
     return set_error(TREX_E_ARG, "%s: empty normaliser (n_valid=%g, n_nonroot=%d)", fn, n_valid,
                      n_nonroot);
@@ -1277,13 +1285,18 @@ extern "C" int trex_nk_landscape_loss(const int32_t* plan, int n_parents, const 
   if (k > 0) launch_logits_bwd(a, ns, st, dlog, G);
   (void)dpar;
   const int64_t glds = (int64_t)L * k * 16;
-  if (v4 && k > 0 && glds <= kNkCombineLds) {
-    static const bool attr = [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(nk_combine4_lds_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNkCombineLds);
-      return true;
-    }();
-    (void)attr;
+  // the LDS-staged combine wants up to kNkCombineLds of dynamic LDS: granted
+  // once per process; a device (or an ARCH build) that refuses it runs the
+  // plain combine instead
+  static const int64_t lds_cap = [] {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(nk_combine4_lds_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kNkCombineLds) ==
+        hipSuccess)
+      return kNkCombineLds;
+    (void)hipGetLastError();
+    return (int64_t)65536;
+  }();
+  if (v4 && k > 0 && glds <= lds_cap) {
     hipLaunchKernelGGL(nk_combine4_lds_kernel, dim3(N), dim3(kNkCombineThreads), (size_t)glds, st,
                        reinterpret_cast<const float4*>(d_seqs_in),
                        reinterpret_cast<const float4*>(dchild), reinterpret_cast<const float4*>(G),

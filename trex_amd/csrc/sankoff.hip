@@ -1333,8 +1333,12 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
     return set_error(TREX_E_ARG, "%s: dp and d_cost are required", fn);
   if (!nonneg_finite_f32(tau))
     return set_error(TREX_E_ARG, "%s: tau must be finite and >= 0 (got %g)", fn, tau);
-  if (workspace_bytes < trex_workspace_bytes(B, L, n_all, Q))
-    return set_error(TREX_E_ARG, "%s: workspace too small", fn);
+  // 4 < Q <= 20: the kept s rows of the fused site kernel are optional -- a
+  // workspace without them (site_srow_offset bytes) makes it recompute them
+  const bool srow_room = workspace_bytes >= trex_workspace_bytes(B, L, n_all, Q);
+  const int64_t min_ws = (Q > 4 && Q <= kSiteMaxQ) ? site_srow_offset(B, L, Q)
+                                                   : trex_workspace_bytes(B, L, n_all, Q);
+  if (workspace_bytes < min_ws) return set_error(TREX_E_ARG, "%s: workspace too small", fn);
   if (n_slots < 0) return set_error(TREX_E_ARG, "%s: bad n_slots", fn);
   if (flags & ~TREX_FLAG_HARD_ROOT) return set_error(TREX_E_ARG, "%s: unknown flags 0x%x", fn, flags);
   // plan info[0]: stack depth | (lane-program slots + 1) << 16
@@ -1381,7 +1385,7 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
       float* kg = reinterpret_cast<float*>(tail - 3456);  // K and K^T
       c.site_flag = flag;
       c.site_kg = kg;
-      if (phase == 3 && site_srow_on())
+      if (phase == 3 && srow_room && site_srow_on())
         c.site_srow = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                                site_srow_offset(B, L, Q));
       if (int e = wide_run(fn, c, /*reduce=*/false)) return e;

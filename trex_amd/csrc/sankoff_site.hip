@@ -281,11 +281,18 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
           __builtin_amdgcn_raw_buffer_store_b128(w[c], r, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 0);
         }
       }
-      // the stores' data registers stay untouched past the last store's issue
-      // (without this the compiler reused the last chunk's registers for the
-      // next VALU result right after the store and a few lanes' bytes landed
-      // corrupted; observed on MI355X, tools/dbg/site_dp2.py)
-      asm volatile("s_nop 4" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]));
+      // gfx950 store-data hazard: a VALU write of a 128-bit store's data VGPR
+      // in the instruction right after the store changes the bytes it writes
+      // -- also with an SGPR soffset, where LLVM inserts no wait state
+      // (tools/micro/store_reuse.hip: 2 % of rows corrupted at distance 1,
+      // none after one s_nop).  One wait state after the last
+      // store, the data registers held live through it so none is
+      // reallocated before it; tests/test_isa_guard_cpu.py checks every
+      // code object of the build for the pattern.
+      asm volatile("s_nop 0" ::: "memory");
+#pragma unroll
+      for (int c = 0; c < kSQ / 4; ++c)
+        if (4 * c < Q) asm volatile("" ::"v"(w[c]));
     } else {
 #pragma unroll
       for (int j = 0; j < kSQ; ++j)

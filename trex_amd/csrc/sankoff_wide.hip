@@ -379,9 +379,10 @@ __global__ __launch_bounds__(kWave, (wide_min_blocks<G, PHASE>())) void sankoff_
       const bool handled = site_takes_call(gmin, gmax, A.a);
       if (blockIdx.x == 0) site_gate_write(A.cost, Q, gmin, A.a, A.site_kg, A.site_flag, handled);
       if (handled) {
-        // the first workgroups build the cherry tables below K
-        __shared__ float kl[kSiteSQ * kSiteSQ + kSiteSQ];
-        site_pair_tables(A.cost, Q, gmin, A.a, A.bcoef, A.site_kg - kSiteTabBytes / 4, kl);
+        // the first workgroups build the cherry tables below K (their
+        // (kSiteSQ + 1) kSiteSQ scratch floats are carved from the dynamic
+        // LDS, which wide_run sizes to hold them on gated launches)
+        site_pair_tables(A.cost, Q, gmin, A.a, A.bcoef, A.site_kg - kSiteTabBytes / 4, lds);
         return;
       }
     }
@@ -771,7 +772,9 @@ int64_t wide_workspace_bytes(int B, int L, int Q) {
 
 int wide_run(const char* fn, const WideCall& c, bool reduce) {
   const int tiles = wide_tiles(c.L, c.Q);
-  const size_t lds = wide_lds_bytes(c.n_slots, c.nl, c.ni, c.Q);
+  size_t lds = wide_lds_bytes(c.n_slots, c.nl, c.ni, c.Q);
+  // a gated launch may build the site kernel's cherry tables in its LDS
+  if (c.site_flag) lds = std::max(lds, (size_t)(kSiteSQ * kSiteSQ + kSiteSQ) * 4);
   if (lds > 65536) return set_error(TREX_E_UNSUPPORTED, "%s: LDS stack too deep", fn);
   if ((int64_t)c.B * tiles > 0x7FFFFFFF) return set_error(TREX_E_ARG, "%s: grid too large", fn);
   if ((int64_t)c.ni * c.L * c.Q * 4 > 0x7FFFFFF0LL)

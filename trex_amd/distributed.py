@@ -60,6 +60,8 @@ class GramReducer:
 
     def __init__(self, group=None):
         self.group = group
+        self.calls = 0  # all-reduces issued and their payload (bench.py reports
+        self.bytes = 0  # the per-step Gram exchange from these)
 
     def __call__(self, G):
         import torch.distributed as dist
@@ -68,6 +70,8 @@ class GramReducer:
             raise ValueError("GramReducer: G (or its row block) must be contiguous")
         if dist.is_available() and dist.is_initialized():
             dist.all_reduce(G, group=self.group)
+            self.calls += 1
+            self.bytes += G.numel() * G.element_size()
         return G
 
 

@@ -164,6 +164,10 @@ class LandscapeAwareLoss:
             os.environ.get("TREX_NK_SPLIT", "1") != "0"
         if self.split:
             self.x3 = K % 16 == 0 and os.environ.get("TREX_NK_X3", "1") != "0"
+            # the x3 GEMMs' contract is |S| <= 1: the ancestor rows are
+            # softmaxes, the leaf rows are the caller's masked_sequences and
+            # are checked whenever they change (_set_leaves)
+            self.x3_allowed = self.x3
             self.G = torch.empty((self.N, self.N), **f32)
             self.M = torch.empty((self.N, self.N), **f32)
             self.m_bound = float(np.abs(A).sum(0).max() + np.abs(A).sum(1).max()
@@ -208,6 +212,16 @@ class LandscapeAwareLoss:
         if refresh or ms is not self._s_src or ver is None or ver != self._s_ver:
             self.S.copy_(ms)
             self._s_src, self._s_ver = ms, ver
+            if self.split and self.x3_allowed:
+                # one-hot / softmax leaves (|S| <= 1) keep the f16x3 GEMMs;
+                # anything larger would overflow their f16 pieces, so those
+                # leaves (and leaves copied while a hipGraph is being
+                # captured, where the check cannot sync) take the f32 GEMMs
+                torch = _torch()
+                if torch.cuda.is_current_stream_capturing():
+                    self.x3 = False
+                else:
+                    self.x3 = bool(self.S[: self.n_leaves].abs().max().item() <= 1.0)
             if self.split:  # the leaf x leaf Gram block of these leaves
                 check(lib().trex_tree_gram(ptr(self.S), self.N, self.L * self.Q, ptr(self.G),
                                            ptr(self.tree_ws), self.tree_ws.numel(),
