@@ -266,7 +266,7 @@ def test_c5_full_size_steps_vs_fp64(device, gemm):
         # data, measured here, and the check is only meaningful if it is rare
         at_cap = float(np.mean(tol >= cap))
         ratios["ancestors at cap"].append(at_cap)
-        assert at_cap < 1e-2, at_cap
+        assert at_cap < 1e-3, at_cap  # measured 5e-5 (step 1) at this size
         del anc, S_anc, g_anc, b, tol, want, new_anc
     print(f"C5 {gemm}: max err / bound per step", {k: [f"{x:.3g}" for x in v]
                                                    for k, v in ratios.items()})

@@ -12,6 +12,7 @@ d=json.load(open(sys.argv[1]))
 extra = ''
 if 'c3' in d: extra += ' c3 soft %.1f us hard %.1f us' % (d['c3']['soft_ms_per_step']*1e3, d['c3']['hard_recon_ms_per_step']*1e3)
 if 'c5' in d: extra += ' c5 %.3f ms' % d['c5']['ms_per_step']
+if 'c5' in d and 'kernels' in d['c5']: extra += ' (gram %.1f mf %.1f us)' % (d['c5']['kernels']['gram']['us'], d['c5']['kernels']['mf']['us'])
 if 'nk' in d: extra += ' nk_dna %.3f ms' % d['nk']['dna_256x2000_q4_k4']['ms_per_step']
 if 'c5_f32' in d: extra += ' c5_f32 %.3f ms' % d['c5_f32']['ms_per_step']
 if 'c4_shard' in d: extra += ' shard %.1f us' % d['c4_shard']['fused_kernel_us']
