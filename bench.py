@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--states", type=int, default=4)
     ap.add_argument("--tau", type=float, default=0.5)
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly, no hipGraph")
+    ap.add_argument("--no-settle", action="store_true",
+                    help="skip the clock-settle steps before the warmup (cold-start timing)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 single-tree line")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 protein line")
@@ -758,6 +760,43 @@ def main():
                     ar_events.append(ev)
                 done[i].record(comm)
 
+    # settle: a fresh box runs the first ~30 ms of sustained work at rising
+    # clocks (per-step 1 084 -> 922 us over the first 35 steps, then flat:
+    # tools/time_step.py, profiles/r06_c4_cold_ramp.txt).  Blocks of 5 steps
+    # (>= 5 ms each) run until one is within 1 % of the one before (at most 20), so
+    # the W warmup and K timed steps below measure the steady state; the
+    # settle steps are reported in the line (config.settle_steps)
+    # (N > 1: the stop decision is all-reduced, so every rank runs the same
+    # steps and issues the same all-reduces)
+    settle = 0
+    if not args.no_settle:
+        prev = None
+        nblk = 5  # steps per block; after the first block, >= 5 ms of steps
+        for blk in range(20):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(nblk):
+                run_once()
+            torch.cuda.synchronize()
+            cur = (time.perf_counter() - t0) / nblk
+            settle += nblk
+            if blk == 0:
+                nb5 = max(5, int(np.ceil(5e-3 / max(cur, 1e-6))))
+                if dist_on:
+                    nbt = torch.tensor([nb5], dtype=torch.int32, device=device)
+                    dist.all_reduce(nbt, op=dist.ReduceOp.MAX)
+                    nb5 = int(nbt.item())
+                nblk = nb5
+                prev = None
+                continue
+            stop = prev is not None and cur >= 0.99 * prev
+            if dist_on:
+                flag = torch.tensor([1 if stop else 0], dtype=torch.int32, device=device)
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                stop = bool(flag.item())
+            if stop:
+                break
+            prev = cur
     for _ in range(args.warmup):
         run_once()
     torch.cuda.synchronize()
@@ -820,7 +859,7 @@ def main():
     dom = "sankoff_fwd_bwd"
     achieved = kern[dom][1] / kern[dom][0] / 1e9
     # measured HBM traffic per launch (rocprofv3 FETCH_SIZE / WRITE_SIZE passes,
-    # calibrated: tools/traffic_passes.sh -> profiles/traffic.json)
+    # calibrated: tools/pmc.sh traffic c4 -> profiles/traffic.json)
     traffic = {}
     try:
         with open(args.traffic) as f:
@@ -859,6 +898,7 @@ def main():
                                   "the next step" if dist_on else ""),
                    "trees": args.trees, "trees_rank0": B, "taxa": n, "sites": L, "states": Q,
                    "tau": tau, "hipgraph": use_graph, "parallelism": f"tree-batch x{world}",
+                   "settle_steps": settle,
                    "process_group": dist.get_backend() if dist_on else None,
                    "rccl_ranks": dist_info["rccl_ranks"] if dist_info else None,
                    "world_size": dist_info["world_size"] if dist_info else None},

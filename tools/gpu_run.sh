@@ -10,9 +10,8 @@
 #   bench[:args]    python bench.py args                     -> TAG_bench.json
 #   prof[:args]     rocprofv3 --kernel-trace --stats of bench.py args
 #                   -> TAG_prof/ (+ TAG_prof_by_grid.txt)
-#   pmc:file        tools/pmc_passes.sh style counter passes listed in file
-#   ab_libs:a.so,b.so   tools/ab_libs.sh over those libraries -> TAG_ab.txt
-#   ab_env:A=1,A=0      tools/ab_env.sh over those settings    -> TAG_ab.txt
+#   pmc:GROUP,WORKLOAD  tools/pmc.sh GROUP WORKLOAD -> TAG_pmc/ (+ TAG_pmc.txt summary)
+#   ab:a.so,b.so | ab:A=1,A=0   tools/ab.sh over those arms -> TAG_ab.txt
 # outputs land in gpurun_out/TAG_*.
 set -o pipefail
 TAG=$1
@@ -46,14 +45,16 @@ for step in "$@"; do
         python3 "$ROOT/tools/kernels_by_grid.py" "$csv" >> "$OUT/${TAG}_prof_by_grid.txt" 2>&1
       done
       cat "$OUT/${TAG}_prof_by_grid.txt" ;;
-    ab_libs)
-      timeout -k 10 900 bash "$ROOT/tools/ab_libs.sh" $arg > "$OUT/${TAG}_ab.txt" 2>&1 \
+    pmc)
+      set -- $arg
+      timeout -k 10 900 bash "$ROOT/tools/pmc.sh" "$1" "$2" "$OUT/${TAG}_pmc" > "$OUT/${TAG}_pmc.log" 2>&1 \
+        || { tail -30 "$OUT/${TAG}_pmc.log"; exit 1; }
+      python3 "$ROOT/tools/pmc_summary.py" "$OUT/${TAG}_pmc" > "$OUT/${TAG}_pmc.txt" 2>&1
+      tail -40 "$OUT/${TAG}_pmc.txt" ;;
+    ab)
+      timeout -k 10 900 bash "$ROOT/tools/ab.sh" $arg > "$OUT/${TAG}_ab.txt" 2>&1 \
         || { tail -30 "$OUT/${TAG}_ab.txt"; exit 1; }
-      cat "$OUT/${TAG}_ab.txt" | tail -20 ;;
-    ab_env)
-      timeout -k 10 900 bash "$ROOT/tools/ab_env.sh" $arg ${REPS:-2} > "$OUT/${TAG}_ab.txt" 2>&1 \
-        || { tail -30 "$OUT/${TAG}_ab.txt"; exit 1; }
-      cat "$OUT/${TAG}_ab.txt" | tail -20 ;;
+      grep -v amdgpu.ids "$OUT/${TAG}_ab.txt" | tail -20 ;;
     *)
       echo "unknown step $name"; exit 2 ;;
   esac

@@ -2,7 +2,7 @@
 
     python tools/pmc_traffic.py PMCDIR CALIBDIR [--out profiles/traffic.json]
 
-PMCDIR holds two rocprofv3 runs of tools/prof_kernels.py, pass_fetch
+PMCDIR holds two rocprofv3 runs of tools/prof.py c4, pass_fetch
 (--pmc FETCH_SIZE) and pass_write (--pmc WRITE_SIZE), counters reported in
 KiB per dispatch.  CALIBDIR holds the same two passes over
 tools/micro/load_pattern and tools/micro/store_pattern, whose byte counts are

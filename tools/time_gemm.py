@@ -1,4 +1,4 @@
-"""HIP-event times of the C5 GEMM kernels (tools/prof_gemm.py shapes) for the
+"""HIP-event times of the C5 GEMM kernels (tools/prof.py gemm shapes) for the
 library TREX_HIP_LIB points at: one line 'gram_us mf_us'."""
 import os
 import sys

@@ -60,7 +60,7 @@ struct SArgs {
 };
 
 #ifdef TREX_STAGED_TIMING
-// diagnostic build (tools/build_diag.sh): wave 0 of each of the first 4096
+// diagnostic build (tools/build_ab.sh stagetime sankoff_staged.hip -DTREX_STAGED_TIMING): wave 0 of each of the first 4096
 // workgroups stamps s_memtime at phase boundaries
 __device__ unsigned long long g_stage_t[4096][20];
 __device__ unsigned long long g_stage_rt[4096][2];  // s_memrealtime (100 MHz) at start / end
