@@ -106,8 +106,9 @@ int trex_plan_build(const int32_t* children, int B, int n_all, int32_t* plan,
  * kernel's gate words, K / K^T and cherry tables.  For 4 < Q <= 20 the value
  * also covers a region the size of the DP table (B * n_int * L * Q * 4 bytes)
  * where the fused call keeps its forward's softmin row sums for its adjoint;
- * a smaller workspace (down to the size without that region) is accepted
- * and the fused kernel then recomputes those sums.  Zero it once with
+ * a smaller workspace, down to the value minus B * n_int * L * Q * 4 bytes,
+ * is accepted and the fused kernel then recomputes those sums (bitwise the
+ * same results).  Zero it once with
  * trex_workspace_init before first use. */
 int64_t trex_workspace_bytes(int B, int L, int n_all, int Q);
 int trex_workspace_init(void* workspace, int64_t workspace_bytes, void* stream);

@@ -344,3 +344,34 @@ def test_site_kernel_shortcuts_are_bitwise_neutral(device, monkeypatch, topo, kn
     ref = batched_fwd_bwd_ref(ch, leaves, cost, tau)
     assert_grad_close(runs[0][3].cpu().numpy(), ref["d_cost"], rtol=cond_rtol(ref["dp"], tau))
     assert_dp_close(_sm(runs[0][0]), ref, SOFT_RTOL)
+
+
+def test_site_kernel_smaller_workspace_recomputes_s_rows_bitwise(device):
+    """the fused lane-per-site call's kept s rows are optional --
+    a workspace of trex_workspace_bytes - B n_int L Q 4 bytes is accepted
+    (the adjoint recomputes s, bitwise the same: the TREX_SITE_SROW=0 path)
+    and one byte less is refused (include/trex_hip.h)."""
+    from trex_amd._lib import TrexError
+
+    B, n, L, Q, tau = 2, 64, 777, 20, 0.5
+    ch = random_topologies(B, n, seed=81)
+    leaves = random_leaves(B, n, L, Q, seed=82, missing=0.03)
+    lv = _dev(leaves, device)
+    c = _dev(int_cost(Q, seed=83), device, torch.float32)
+    eng = _engine(ch, L, Q, device)
+    f, dc, mg, _ = eng.fwd_bwd(lv, c, tau, marginals=True)
+    ref = (f.dp.clone(), f.tree_score.clone(), dc.clone(), mg.clone())
+    n_int = n - 1  # n taxa: 2n - 1 nodes, n - 1 internal rows
+    small = eng.workspace.numel() - B * n_int * L * Q * 4
+    full = eng.workspace
+    try:
+        eng.workspace = full[:small]
+        f2, dc2, mg2, _ = eng.fwd_bwd(lv, c, tau, marginals=True)
+        torch.cuda.synchronize()
+        assert torch.equal(f2.dp, ref[0]) and torch.equal(f2.tree_score, ref[1])
+        assert torch.equal(dc2, ref[2]) and torch.equal(mg2, ref[3])
+        eng.workspace = full[:small - 1]
+        with pytest.raises(TrexError):
+            eng.fwd_bwd(lv, c, tau)
+    finally:
+        eng.workspace = full

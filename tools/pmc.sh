@@ -23,6 +23,7 @@ else
 fi
 pass() {  # pass NAME "COUNTERS" [command]
   local c=${3:-$CMD}
+  mkdir -p "$(dirname "$OUT/$1")"
   timeout -s KILL ${PASS_TIMEOUT:-150} rocprofv3 --kernel-trace --pmc $2 -d "$OUT/$1" -o run \
     --output-format csv -- $c > "$OUT/$1.log" 2>&1
 }
