@@ -3,7 +3,7 @@ softmin fwd + grad) and C3 (64 taxa x 10 000 x 20, fwd + grad + marginals +
 soft ancestral) under kernel-selection environment settings, hipGraph
 replay (what bench.py's c2 / c3 lines time).
 
-  python tools/time_small.py [C2|C3|C1] ...   (default: C2 C3)
+  python tools/time_small.py [C2|C3|C3P] ...   (default: C2 C3)
 """
 
 from __future__ import annotations
@@ -28,6 +28,13 @@ CONFIGS = {
            ("staged", {"TREX_WIDE_SMALLQ": "1", "TREX_STAGED": "1"}),
            ("lane", {"TREX_WIDE_SMALLQ": "0", "TREX_STAGED": "0"})],
     "C3": [("wave", {"TREX_STAGED": "0"}), ("staged", {"TREX_STAGED": "1"})],
+    # the lane-per-site kernel: one wave per site set vs a wave pair (sankoff_site2.hip)
+    "C3P": [("one", {"TREX_SITE2": "0"}), ("pair8", {"TREX_SITE2": "8"}),
+            ("pair6", {"TREX_SITE2": "6"}), ("pair4", {"TREX_SITE2": "4"}),
+            ("one", {"TREX_SITE2": "0"}), ("pair8", {"TREX_SITE2": "8"}),
+            ("pair6", {"TREX_SITE2": "6"}), ("pair4", {"TREX_SITE2": "4"})],
+    "C3Q": [("one", {"TREX_SITE2": "0"}), ("pair8", {"TREX_SITE2": "8"}),
+            ("one", {"TREX_SITE2": "0"}), ("pair8", {"TREX_SITE2": "8"})],
 }
 
 
@@ -54,6 +61,7 @@ def replay_us(fn, n=100, per_graph=10):
 
 
 def case(name, dev):
+    name = name[:2]
     if name == "C2":
         nl, L, Q, tau, mut, seed = 64, 10000, 4, 1.0, 5, 1
         cost = (np.ones((Q, Q)) - np.eye(Q)).astype(np.float32)
@@ -95,7 +103,11 @@ def main():
             if ref is None:
                 ref = (sc, dc)
             rel = float(np.abs(dc - ref[1]).max() / np.abs(ref[1]).max())
-            print(f"{name} {label:7s} {us:8.1f} us  score {sc:.6f}  dC rel diff {rel:.2e}",
+            extra_s = ""
+            if "TREX_SITE2" in env:
+                from trex_amd._lib import lib
+                extra_s = f"  site2 launches {lib().trex_debug_site2_launches()}"
+            print(f"{name} {label:7s} {us:8.1f} us  score {sc:.6f}  dC rel diff {rel:.2e}{extra_s}",
                   flush=True)
 
 

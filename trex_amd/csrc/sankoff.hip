@@ -1389,7 +1389,9 @@ int run_phase(const char* fn, int phase, const int32_t* plan, int n_slots, const
         c.site_srow = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                                site_srow_offset(B, L, Q));
       if (int e = wide_run(fn, c, /*reduce=*/false)) return e;
-      if (int e = site_run(fn, c, lanes, lp_slots, flag, kg)) return e;
+      if (int e = site2_on(lp_slots, c.nl, c.ni) ? site2_run(fn, c, lanes, lp_slots, flag, kg)
+                                                 : site_run(fn, c, lanes, lp_slots, flag, kg))
+        return e;
       return partial_reduce(fn, static_cast<double*>(workspace),
                             static_cast<double*>(workspace) + (int64_t)B * wide_tiles(L, Q), B,
                             wide_tiles(L, Q), Q, phase, tree_score, d_cost, stream, nullptr, 0, 0,

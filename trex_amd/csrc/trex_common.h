@@ -168,6 +168,11 @@ inline int64_t site_srow_offset(int B, int L, int Q) {
 int site_tiles(int L);
 int site_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots,
              const int* flag, const float* kg);
+// the same with each site's states split over a wave pair (sankoff_site2.hip;
+// TREX_SITE2=1 / 8 / 6 / 4, read per call: the pair count, when its LDS fits)
+bool site2_on(int lp_slots, int nl, int ni);
+int site2_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_slots,
+              const int* flag, const float* kg);
 int wide_backtrack(const int32_t* bt, const float* cost, const float* dp, int B, int L, int ni,
                    int Q, int8_t* anc, void* stream);
 int wide_ragged_backtrack(const int32_t* rmeta, int B, int64_t items, int64_t steps,
