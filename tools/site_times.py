@@ -1,8 +1,10 @@
 """Phase timestamps of the lane-per-site kernel (diagnostic build:
 tools/build_ab.sh sitet sankoff_site.hip -DTREX_SITE_TIMING) on C3: per wave
-and phase, mean cycles over workgroups.
+and phase, mean cycles over workgroups.  --pair: the wave-pair kernel
+(tools/build_ab.sh s2t sankoff_site2.hip -DTREX_SITE2_TIMING, 16 waves).
 
   TREX_HIP_LIB=trex_amd/libtrex_ab_sitet.so python tools/site_times.py
+  TREX_HIP_LIB=trex_amd/libtrex_ab_s2t.so python tools/site_times.py --pair
 """
 import ctypes
 import os
@@ -14,7 +16,11 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-os.environ.setdefault("TREX_HIP_LIB", os.path.join(ROOT, "trex_amd", "libtrex_ab_sitet.so"))
+PAIR = "--pair" in sys.argv
+if PAIR:
+    os.environ.setdefault("TREX_SITE2", "8")
+os.environ.setdefault("TREX_HIP_LIB", os.path.join(ROOT, "trex_amd",
+                                                   "libtrex_ab_s2t.so" if PAIR else "libtrex_ab_sitet.so"))
 from _cases import int_cost, simulate_leaves  # noqa: E402
 
 from trex_amd import SankoffEngine, TreePlan, children_from_adjacency  # noqa: E402
@@ -29,8 +35,9 @@ c = torch.as_tensor(int_cost(Q, seed=3), device=dev)
 for _ in range(10):
     eng.fwd_bwd(lv, c, tau, marginals=True, anc_states=True)
 torch.cuda.synchronize()
-buf = np.zeros((2048, 8, 20), np.uint64)
-fn = lib().trex_debug_site_times
+NW = 16 if PAIR else 8
+buf = np.zeros((2048, NW, 20), np.uint64)
+fn = lib().trex_debug_site2_times if PAIR else lib().trex_debug_site_times
 fn.argtypes = [ctypes.c_void_p]
 assert fn(buf.ctypes.data) == 0
 nwg = (L + 63) // 64
@@ -46,5 +53,5 @@ for j in range(1, 17):
     if not col.any():
         continue
     d = col - prev
-    print(f"{names[j]:12s} " + " ".join(f"{d[:, w].mean():8.0f}" for w in range(8)))
+    print(f"{names[j]:12s} " + " ".join(f"{d[:, w].mean():7.0f}" for w in range(NW)))
     prev = col

@@ -3,7 +3,7 @@ softmin fwd + grad) and C3 (64 taxa x 10 000 x 20, fwd + grad + marginals +
 soft ancestral) under kernel-selection environment settings, hipGraph
 replay (what bench.py's c2 / c3 lines time).
 
-  python tools/time_small.py [C2|C3|C3P] ...   (default: C2 C3)
+  python tools/time_small.py [C2|C3|C3P|C3Q] ...   (default: C2 C3)
 """
 
 from __future__ import annotations
@@ -61,7 +61,6 @@ def replay_us(fn, n=100, per_graph=10):
 
 
 def case(name, dev):
-    name = name[:2]
     if name == "C2":
         nl, L, Q, tau, mut, seed = 64, 10000, 4, 1.0, 5, 1
         cost = (np.ones((Q, Q)) - np.eye(Q)).astype(np.float32)
@@ -69,7 +68,9 @@ def case(name, dev):
         nl, L, Q, tau, mut, seed = 64, 10000, 20, 0.5, 50, 2
         cost = int_cost(Q, seed=3)
     seqs, adj = simulate_leaves(nl, L, Q, mut, seed=seed)
-    eng = SankoffEngine(TreePlan(children_from_adjacency(adj)), L, Q, dev)
+    ch = children_from_adjacency(adj)
+    name = name[:2]
+    eng = SankoffEngine(TreePlan(ch), L, Q, dev)
     lv = torch.from_numpy(np.ascontiguousarray(seqs[None, :nl])).to(dev)
     c = torch.from_numpy(cost).to(dev)
     f = torch.empty(eng.dp_shape, dtype=torch.float32, device=dev)

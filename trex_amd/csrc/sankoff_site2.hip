@@ -88,6 +88,22 @@ struct Site2Args {
   int n_slots;
 };
 
+#ifdef TREX_SITE2_TIMING
+// diagnostic build (tools/build_ab.sh s2t sankoff_site2.hip -DTREX_SITE2_TIMING):
+// lane 0 of every wave of the first 2048 workgroups stamps s_memtime at the
+// phase boundaries of sankoff_site.hip's SITE_STAMP (tools/site_times.py --pair)
+__device__ unsigned long long g_site2_t[2048][16][20];
+#define SITE2_STAMP(j)                                                             \
+  do {                                                                             \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048 && (j) < 20)                  \
+      g_site2_t[blockIdx.x][threadIdx.x >> 6][j] = __builtin_amdgcn_s_memtime();  \
+  } while (0)
+#else
+#define SITE2_STAMP(j) \
+  do {                 \
+  } while (0)
+#endif
+
 __device__ __forceinline__ void site2_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -110,6 +126,7 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
   constexpr bool BWD = (PHASE & 2) != 0;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   if (!__builtin_amdgcn_readfirstlane(as_const(A.flag)[0])) return;
+  SITE2_STAMP(0);
   const int Q = QC ? QC : A.Q;
   const int ni = A.n_int;
   const int L = A.L;
@@ -223,6 +240,7 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
     }
   }
   __syncthreads();
+  SITE2_STAMP(1);
 
   auto pword = [&](int e) { return __builtin_amdgcn_readfirstlane(lprog[e]); };
   const int S = pword(0);
@@ -248,9 +266,16 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
   // instruction 1 KiB contiguous (sankoff_site.hip store_row)
   auto store_row = [&](rsrc_t r, int row, const float (&v)[kH]) {
     pair_sync();  // the partner is done reading xr
+    if (QC == kSQ2) {
+      // 8-byte aligned pairs (Q and s0 even)
 #pragma unroll
-    for (int k = 0; k < kH; ++k)
-      if (valid(k)) xr[lane * Q + s0 + k] = v[k];
+      for (int k = 0; k < kH; k += 2)
+        *reinterpret_cast<float2*>(xr + lane * Q + s0 + k) = make_float2(v[k], v[k + 1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kH; ++k)
+        if (valid(k)) xr[lane * Q + s0 + k] = v[k];
+    }
     pair_sync();
     const int npieces = Q * kWave * 4 / 16;  // Q * 16
     const bool q4 = (Q & 3) == 0;
@@ -283,19 +308,70 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
     }
   };
   const int vbase = active ? site * Q * 4 : 0x7FFFFFF0;
+  // direct (lane-strided) row I/O of this wave's 10 states: at Q = 20 as
+  // 16 + 16 + 8 bytes (states 0-3, 4-7, 8-9 | 10-11, 12-15, 16-19; a site's
+  // row starts 16-byte aligned): three accesses where 4-byte ones would touch
+  // every site's cache line ten times
+  auto u4 = [](float a0, float a1, float a2, float a3) {
+    return u32x4{__float_as_uint(a0), __float_as_uint(a1), __float_as_uint(a2), __float_as_uint(a3)};
+  };
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
   auto store_row_direct = [&](rsrc_t r, int row, const float (&v)[kH]) {
+    if constexpr (QC == kSQ2) {
+      const uint32_t so = row * rowbytes;
+      if (hf == 0) {
+        const u32x4 w0 = u4(v[0], v[1], v[2], v[3]), w1 = u4(v[4], v[5], v[6], v[7]);
+        const u32x2 w2 = u32x2{__float_as_uint(v[8]), __float_as_uint(v[9])};
+        __builtin_amdgcn_raw_buffer_store_b128(w0, r, vbase, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(w1, r, vbase + 16, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(w2, r, vbase + 32, so, 0);
+        // gfx950 store-data hazard
+        asm volatile("s_nop 0" ::: "memory");
+        asm volatile("" ::"v"(w0), "v"(w1), "v"(w2));
+      } else {
+        const u32x2 w0 = u32x2{__float_as_uint(v[0]), __float_as_uint(v[1])};
+        const u32x4 w1 = u4(v[2], v[3], v[4], v[5]), w2 = u4(v[6], v[7], v[8], v[9]);
+        __builtin_amdgcn_raw_buffer_store_b64(w0, r, vbase + 40, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(w1, r, vbase + 48, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(w2, r, vbase + 64, so, 0);
+        asm volatile("s_nop 0" ::: "memory");
+        asm volatile("" ::"v"(w0), "v"(w1), "v"(w2));
+      }
+    } else {
 #pragma unroll
-    for (int k = 0; k < kH; ++k)
-      if (valid(k))
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[k]), r, vbase + 4 * (s0 + k),
-                                              row * rowbytes, 0);
+      for (int k = 0; k < kH; ++k)
+        if (valid(k))
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[k]), r, vbase + 4 * (s0 + k),
+                                                row * rowbytes, 0);
+    }
   };
   auto load_row_r = [&](rsrc_t rr, int row, float (&v)[kH]) {
+    if constexpr (QC == kSQ2) {
+      const uint32_t so = row * rowbytes;
+      u32x4 a, b;
+      u32x2 c;
+      if (hf == 0) {
+        a = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase, so, 1);
+        b = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 16, so, 1);
+        c = __builtin_amdgcn_raw_buffer_load_b64(rr, vbase + 32, so, 1);
+        const uint32_t x[kH] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y};
 #pragma unroll
-    for (int k = 0; k < kH; ++k)
-      v[k] = valid(k) ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, vbase + 4 * (s0 + k),
-                                                                             row * rowbytes, 1))
-                      : 0.0f;
+        for (int k = 0; k < kH; ++k) v[k] = __uint_as_float(x[k]);
+      } else {
+        c = __builtin_amdgcn_raw_buffer_load_b64(rr, vbase + 40, so, 1);
+        a = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 48, so, 1);
+        b = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 64, so, 1);
+        const uint32_t x[kH] = {c.x, c.y, a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < kH; ++k) v[k] = __uint_as_float(x[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kH; ++k)
+        v[k] = valid(k) ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, vbase + 4 * (s0 + k),
+                                                                               row * rowbytes, 1))
+                        : 0.0f;
+    }
   };
   auto load_row = [&](int row, float (&v)[kH]) { load_row_r(rdp, row, v); };
   auto slot_get = [&](int sl, float (&v)[kH]) {
@@ -469,6 +545,7 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
         }
       }
       site2_barrier();
+      SITE2_STAMP(2 + (s < 5 ? s : 5));
     }
   }
 
@@ -531,8 +608,10 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
   }
 
   if constexpr (BWD) {
+    SITE2_STAMP(8);
     if constexpr (FWD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    SITE2_STAMP(9);
     // dC accumulators on v_mfma_f32_16x16x32_bf16, split by rows between
     // the pair: wave hf owns parent states i in [16 hf, 16 hf + 16) (rows
     // >= 20 discarded) over all 64 sites, two 16-column tiles (j < 32);
@@ -802,6 +881,7 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
         adj_task(load_step(steps, lo + (split ? it >> 1 : it)), c_lo, split ? c_lo + 1 : 2);
       }
       site2_barrier();
+      SITE2_STAMP(10 + (S - 1 - s < 5 ? S - 1 - s : 5));
     }
 
     // ---- dC partial: dC_ij = K_ij acc1_ij + acc2_ij per pair, the 8 pairs
@@ -826,6 +906,7 @@ __global__ __launch_bounds__(2 * NP * kWave, 1) void sankoff_site2_kernel(Site2A
       for (int w = 1; w < kPairs; ++w) tsum += red[(size_t)w * Q2 + e];
       A.part_dc[(size_t)e * nb + blockIdx.x] = tsum;
     }
+    SITE2_STAMP(16);
   }
 }
 
@@ -930,6 +1011,12 @@ int site2_run(const char* fn, const WideCall& c, const int32_t* lanes, int lp_sl
 }
 
 }  // namespace trex
+
+#ifdef TREX_SITE2_TIMING
+extern "C" int trex_debug_site2_times(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(trex::g_site2_t), sizeof(trex::g_site2_t)) == hipSuccess ? 0 : -4;
+}
+#endif
 
 // launches of the wave-pair kernel so far (tests check that TREX_SITE2 took effect)
 extern "C" int trex_debug_site2_launches(void) { return trex::g_site2_launches; }
