@@ -113,6 +113,18 @@ __device__ __forceinline__ void cost_range(const float* __restrict__ cost_, floa
   cmax = uniform(cmax);
 }
 
+// C == C^T (then K == K^T), wave-uniform
+template <int Q>
+__device__ __forceinline__ bool cost_symmetric(const float* __restrict__ cost_) {
+  const cptr<float> cost = as_const(cost_);
+  bool sym = true;
+#pragma unroll
+  for (int i = 0; i < Q; ++i)
+#pragma unroll
+    for (int j = i + 1; j < Q; ++j) sym = sym && cost[i * Q + j] == cost[j * Q + i];
+  return sym;
+}
+
 template <int Q, int MODE>
 __device__ __forceinline__ void load_coef(const float* __restrict__ cost_, float a, Coef<Q>& cf) {
   float cmax;
@@ -305,10 +317,36 @@ __device__ __forceinline__ void bld_row(rsrc_t r, int voff, int soff, float (&d)
   }
 }
 
+// s_i = sum_j K_ij u_j for every parent state i.  SYM (K = K^T, symmetric
+// C): s_i = sum_j K_ji u_j, accumulated over j with the row pairs (K_j,2p,
+// K_j,2p+1) already in SGPRs -- Q / 2 v_pk_fma_f32 per j (8 at Q = 4) instead
+// of a pair-wise dot per i (12)
+template <int Q, bool SYM>
+__device__ __forceinline__ void kvec(const Coef<Q>& cf, const float (&u)[Q], float (&sv)[Q]) {
+  if constexpr (SYM && Q % 2 == 0) {
+    f2 acc[Q / 2];
+#pragma unroll
+    for (int p = 0; p < Q / 2; ++p) acc[p] = pk(cf.k[0][2 * p], cf.k[0][2 * p + 1]) * pk(u[0], u[0]);
+#pragma unroll
+    for (int j = 1; j < Q; ++j)
+#pragma unroll
+      for (int p = 0; p < Q / 2; ++p)
+        acc[p] = __builtin_elementwise_fma(pk(cf.k[j][2 * p], cf.k[j][2 * p + 1]), pk(u[j], u[j]), acc[p]);
+#pragma unroll
+    for (int p = 0; p < Q / 2; ++p) {
+      sv[2 * p] = acc[p].x;
+      sv[2 * p + 1] = acc[p].y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < Q; ++i) sv[i] = kdot<Q>(cf.k[i], u);
+  }
+}
+
 // --------------------------------------------------------------------------
 // message M_c[i] = min_j / smin_j (C[i][j] + D_c[j])      (sankoff.py:67-68)
 // --------------------------------------------------------------------------
-template <int Q, int SPT, int MODE>
+template <int Q, int SPT, int MODE, bool SYM = false>
 __device__ __forceinline__ void message(const Coef<Q>& cf, float a, float bcoef,
                                         const float (&d)[Q][SPT], float (&m)[Q][SPT]) {
   if constexpr (MODE == kHard) {
@@ -332,8 +370,10 @@ __device__ __forceinline__ void message(const Coef<Q>& cf, float a, float bcoef,
 #pragma unroll
       for (int j = 0; j < Q; ++j) u[j] = fast_exp2(fmaf(-d[j][s], a, mda));
       const float base = md + cf.cmin;
+      float sv[Q];
+      kvec<Q, SYM>(cf, u, sv);
 #pragma unroll
-      for (int i = 0; i < Q; ++i) m[i][s] = fmaf(-bcoef, fast_log2(kdot<Q>(cf.k[i], u)), base);
+      for (int i = 0; i < Q; ++i) m[i][s] = fmaf(-bcoef, fast_log2(sv[i]), base);
     }
   } else {
 #pragma unroll
@@ -361,7 +401,7 @@ __device__ __forceinline__ void message(const Coef<Q>& cf, float a, float bcoef,
 // In the factored softmin acc holds sum r_i u_j; the K[i][j] factor is
 // applied once in the final reduction.
 // --------------------------------------------------------------------------
-template <int Q, int SPT, int MODE>
+template <int Q, int SPT, int MODE, bool SYM = false>
 __device__ __forceinline__ void message_adjoint(const Coef<Q>& cf, float a,
                                                 const float (&d)[Q][SPT],
                                                 const float (&g)[Q][SPT],
@@ -401,8 +441,10 @@ __device__ __forceinline__ void message_adjoint(const Coef<Q>& cf, float a,
 #pragma unroll
       for (int j = 0; j < Q; ++j) u[j] = fast_exp2(fmaf(-d[j][s], a, mda));
       float r[Q];
+      float sv[Q];
+      kvec<Q, SYM>(cf, u, sv);
 #pragma unroll
-      for (int i = 0; i < Q; ++i) r[i] = g[i][s] * __builtin_amdgcn_rcpf(kdot<Q>(cf.k[i], u));
+      for (int i = 0; i < Q; ++i) r[i] = g[i][s] * __builtin_amdgcn_rcpf(sv[i]);
 #pragma unroll
       for (int i = 0; i < Q; ++i) axpy<Q>(acc[i], r[i], u);
       // t[j] = sum_i r_i K[i][j] (row pairs of K), gc = u * t
@@ -557,7 +599,7 @@ constexpr int kPrefetchRows = 64;  // leaf tiles of <= 64 leaves are prefetched
 // in LDS, no adjoint re-read, one wave per SIMD -- measured 2.3x slower on the
 // C4 shard and on par for C2; removed in round 3 with the other A/B-only
 // variants)
-template <int Q, int SPT, int MODE, int PHASE, bool RAGGED>
+template <int Q, int SPT, int MODE, int PHASE, bool RAGGED, bool SYM = false>
 __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
   static_assert(!RAGGED || SPT == 1, "ragged batches use the SPT=1 kernels");
   constexpr bool SOFT = MODE != kHard;
@@ -766,7 +808,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
               for (int s = 0; s < SPT; ++s) m[i][s] = d[c][i][s];
           } else {
-            message<Q, SPT, MODE>(cf, a, bcoef, d[c], m);
+            message<Q, SPT, MODE, SYM>(cf, a, bcoef, d[c], m);
           }
 #pragma unroll
           for (int i = 0; i < Q; ++i)
@@ -881,7 +923,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
             }
           }
           float gc[Q][SPT];
-          message_adjoint<Q, SPT, MODE>(cf, a, dc, g, acc, gc);
+          message_adjoint<Q, SPT, MODE, SYM>(cf, a, dc, g, acc, gc);
 #pragma unroll
           for (int i = 0; i < Q; ++i)
 #pragma unroll
@@ -932,7 +974,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
                 for (int s = 0; s < SPT; ++s) gc[j][s] = g[j][s];
             } else {
-              message_adjoint<Q, SPT, MODE>(cf, a, cd[c], g, acc, gc);
+              message_adjoint<Q, SPT, MODE, SYM>(cf, a, cd[c], g, acc, gc);
             }
             if (desc & kChildPrev) {
 #pragma unroll
@@ -1021,9 +1063,14 @@ void sankoff_kernel(KArgs A) {
   } else {
     float cmin, cmax;
     cost_range<Q>(A.cost, cmin, cmax);
-    if (use_ktrick(cmin, cmax, A.a))
-      sankoff_body<Q, SPT, kSoftK, PHASE, RAGGED>(A, lds);
-    else
+    if (use_ktrick(cmin, cmax, A.a)) {
+#ifndef TREX_NO_KSYM
+      if (cost_symmetric<Q>(A.cost))
+        sankoff_body<Q, SPT, kSoftK, PHASE, RAGGED, true>(A, lds);
+      else
+#endif
+        sankoff_body<Q, SPT, kSoftK, PHASE, RAGGED>(A, lds);
+    } else
       sankoff_body<Q, SPT, kSoftDirect, PHASE, RAGGED>(A, lds);
   }
 }
