@@ -1065,7 +1065,9 @@ void sankoff_kernel(KArgs A) {
     cost_range<Q>(A.cost, cmin, cmax);
     if (use_ktrick(cmin, cmax, A.a)) {
 #ifndef TREX_NO_KSYM
-      if (cost_symmetric<Q>(A.cost))
+      // the adjoint-bearing kernels (the forward-only one measured no gain
+      // and would carry a third body's scalar registers: 154 -> 245 spilled)
+      if ((PHASE & 2) && cost_symmetric<Q>(A.cost))
         sankoff_body<Q, SPT, kSoftK, PHASE, RAGGED, true>(A, lds);
       else
 #endif
