@@ -371,6 +371,15 @@ int trex_tree_split_x3(const float* X, int rows, int cols, int ldx, float max_ab
                        int ldo, void* stream);
 int trex_tree_gram_skip_x3p(const void* S16, int N, int64_t K, int skip_rows, float max_abs,
                             float* G, void* workspace, int64_t workspace_bytes, void* stream);
+/* trex_tree_gram_skip_x3p_codes: the same Gram with rows [0, 32 (n_leaf / 32))
+ * declared exact one-hot by their codes (the buffer trex_tree_leaf_codes
+ * filled, status 0; Q = 4): their f16 lo plane is zero, so the lo x hi
+ * products of those strips are skipped -- bitwise trex_tree_gram_skip_x3p.
+ * tree.py:199-209 (the surrogate's S S^T).  Round 6. */
+int trex_tree_gram_skip_x3p_codes(const void* S16, int N, int64_t K, int skip_rows, float max_abs,
+                                  const void* codes, int64_t codes_bytes, int n_leaf, int Q,
+                                  float* G, void* workspace, int64_t workspace_bytes,
+                                  void* stream);
 int trex_tree_mf_rows_x3p(const void* M16, int ldm, const void* S16, int N, int64_t K, int row0,
                           int nrows, float max_abs_m, float max_abs_s, const void* codes,
                           int64_t codes_bytes, int n_leaf, int Q, float* dS_rows, void* stream);

@@ -103,6 +103,14 @@ def test_presplit_and_fused_step_entries_reject_bad_args(bad):
     assert L.trex_tree_split_x3(p, 64, 256, 256, bad, p, 256, None) == TREX_E_ARG
     assert L.trex_tree_split_x3(p, 64, 256, 256, 1.0, p, 254, None) == TREX_E_ARG  # ldo % 4
     assert L.trex_tree_gram_skip_x3p(p, 64, 256, 0, bad, p, w.ctypes.data, ws, None) == TREX_E_ARG
+    assert L.trex_tree_gram_skip_x3p_codes(p, 64, 256, 0, bad, p, 4096, 32, 4, p, w.ctypes.data,
+                                           ws, None) == TREX_E_ARG
+    assert L.trex_tree_gram_skip_x3p_codes(p, 64, 256, 0, 1.0, None, 4096, 32, 4, p,
+                                           w.ctypes.data, ws, None) == TREX_E_ARG  # no codes
+    assert L.trex_tree_gram_skip_x3p_codes(p, 64, 256, 0, 1.0, p, 4096, 32, 5, p, w.ctypes.data,
+                                           ws, None) == TREX_E_ARG  # Q = 4 only
+    assert L.trex_tree_gram_skip_x3p_codes(p, 64, 256, 0, 1.0, p, 100, 32, 4, p, w.ctypes.data,
+                                           ws, None) == TREX_E_ARG  # codes buffer too small
     assert L.trex_tree_mf_rows_x3p(p, 64, p, 64, 256, 0, 64, bad, 1.0, None, 0, 32, 4, p,
                                    None) == TREX_E_ARG
     assert L.trex_tree_mf_rows_x3p(p, 64, p, 64, 258, 0, 64, 65.0, 1.0, None, 0, 32, 4, p,

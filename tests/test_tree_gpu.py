@@ -494,6 +494,39 @@ def _onehot_case(N, L, seed, Q=4):
     return S.reshape(N, L * Q).astype(np.float32), nl
 
 
+@pytest.mark.parametrize("N,L,skip", [(511, 1001, 256), (511, 2048, 0), (300, 257, 128),
+                                      (101, 77, 0), (127, 50, 64)])
+def test_leaf_code_gram_is_bitwise_the_x3p_gram(device, N, L, skip):
+    """trex_tree_gram_skip_x3p_codes (the leaf strips' zero lo-plane
+    products skipped) == trex_tree_gram_skip_x3p bit for bit -- skipped and
+    un-skipped leaf x leaf tiles, n_leaf not a multiple of 32 (N = 101: 51
+    leaves, one code strip), a ragged last K chunk -- and vs fp64."""
+    from trex_amd._lib import check, lib, ptr, stream_handle
+
+    Sn, nl = _onehot_case(N, L, 3 * N + L)
+    K = L * 4
+    S = _t(Sn, device)
+    st = stream_handle(torch.device(device))
+    cb = torch.empty(int(lib().trex_tree_leaf_codes_bytes(nl, L)), dtype=torch.uint8, device=device)
+    status = torch.zeros(1, dtype=torch.int32, device=device)
+    check(lib().trex_tree_leaf_codes(ptr(S), nl, L, 4, ptr(cb), cb.numel(), ptr(status), st))
+    assert int(status.item()) == 0
+    S16 = torch.empty_like(S)
+    check(lib().trex_tree_split_x3(ptr(S), N, K, K, 1.0, ptr(S16), K, st))
+    nbytes = int(lib().trex_tree_workspace_bytes(N, K))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    Ga = torch.zeros((N, N), device=device)
+    Gb = torch.zeros((N, N), device=device)
+    check(lib().trex_tree_gram_skip_x3p(ptr(S16), N, K, skip, 1.0, ptr(Ga), ptr(ws), nbytes, st))
+    check(lib().trex_tree_gram_skip_x3p_codes(ptr(S16), N, K, skip, 1.0, ptr(cb), cb.numel(), nl,
+                                              4, ptr(Gb), ptr(ws), nbytes, st))
+    torch.cuda.synchronize()
+    assert torch.equal(Ga, Gb)
+    t0 = (skip // 64) * 64
+    S64 = Sn.astype(np.float64)
+    assert_grad_close(_n(Gb)[t0:], S64[t0:] @ S64.T, rtol=1e-5, what="G")
+
+
 @pytest.mark.parametrize("N,L", [(511, 1001), (511, 2048), (255, 333), (383, 64), (127, 50),
                                  (101, 77)])
 def test_leaf_code_mf_is_bitwise_the_x3_mf(device, N, L):

@@ -98,6 +98,8 @@ SIGNATURES = {
                                               _c_i, _p, _p]),
     "trex_tree_split_x3": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _p, _c_i, _p]),
     "trex_tree_gram_skip_x3p": (_c_i, [_p, _c_i, _c_i64, _c_i, _c_f, _p, _p, _c_i64, _p]),
+    "trex_tree_gram_skip_x3p_codes": (_c_i, [_p, _c_i, _c_i64, _c_i, _c_f, _p, _c_i64, _c_i,
+                                             _c_i, _p, _p, _c_i64, _p]),
     "trex_tree_mf_rows_x3p": (_c_i, [_p, _c_i, _p, _c_i, _c_i64, _c_i, _c_i, _c_f, _c_f, _p,
                                      _c_i64, _c_i, _c_i, _p, _p]),
     "trex_adam_seq_update_step_x3p": (_c_i, [_p, _c_i, _c_i, _c_i, _c_f, _c_f, _p, _p, _p, _c_i,

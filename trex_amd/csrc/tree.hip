@@ -505,7 +505,7 @@ __device__ __forceinline__ void g3_stage(unsigned char* buf, int row, int sub, c
 template <bool PRE = false>  // PRE: S pre-split (split_x3_group layout)
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gram_kernel3(
     const float* __restrict__ S, int N, int K, int ns, int t0s, int ntiles, int ngroups,
-    int ksplit, int nchunks, float sc, float* __restrict__ part) {
+    int ksplit, int nchunks, float sc, float* __restrict__ part, int lzs = 0) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds3[];
   const int g = blockIdx.x % ngroups;
   const int split = blockIdx.x / ngroups;
@@ -518,7 +518,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int nt = max(0, min(kG3Tiles, ntiles - tb));
   // first tile's strips; tiles past the wave's range (t >= nt) run on
   // whatever strips follow (clamped to ns - 1) and are not written: every
-  // wave issues the same unconditional MFMA stream
+  // wave issues the same unconditional MFMA stream.  (Spreading the leaf
+  // strips' 2-MFMA tiles evenly over the SIMDs measured no gain, PERFLOG.)
   int a0, b0;
   pair_tiles(min(tb, ntiles - 1), ns, 1, t0s, &a0, &b0);
 
@@ -558,6 +559,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     h8 bl = *reinterpret_cast<const h8*>(buf + b * (32 * kG3Stride) + lofs + 32);
 #pragma unroll
     for (int t = 0; t < kG3Tiles; ++t) {
+      // strips a < lzs: exact one-hot leaf rows, whose lo plane is zero
+      const bool zlo = a < lzs;
       if (a != ap) {
         const unsigned char* pa = buf + a * (32 * kG3Stride) + lofs;
         ah = *reinterpret_cast<const h8*>(pa);
@@ -574,7 +577,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         bln = *reinterpret_cast<const h8*>(pb + 32);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the prefetch reads above the MFMAs
-      acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
+      // a zero lo plane adds exact zeros: its MFMA is skipped (bitwise)
+      if (!zlo) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[t], 0, 0, 0);
       bh = bhn;
       bl = bln;
       a = an;
@@ -1293,7 +1299,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         *reinterpret_cast<uint2*>(buf + lofs[j]) =
             uint2{(code == 0 ? hb : 0u) | ((code == 1 ? hb : 0u) << 16),
                   (code == 2 ? hb : 0u) | ((code == 3 ? hb : 0u) << 16)};
+        // the lo plane (zero) is not staged: compute skips its products
+#ifdef TREX_NO_LZ
         *reinterpret_cast<uint2*>(buf + FPLANE + lofs[j]) = uint2{0u, 0u};
+#endif
       }
     }
 #pragma unroll
@@ -1344,6 +1353,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float unscale = 1.0f / (sm * sf);
   auto compute = [&](const unsigned char* buf) {
     const unsigned char* pa = buf + FBUF + (wave * 32 + r) * kMfStride + 16 * h;
+    // leaf-code stages: F's lo plane is zero (one-hot x sf is exact in f16),
+    // so its ah x bl products -- exact zeros -- are skipped (bitwise)
+#ifdef TREX_NO_LZ
+    const bool zlo = false;  // A/B: every product computed
+#else
+    const bool zlo = CODES && cs < lcs;
+#endif
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const h8 ah = *reinterpret_cast<const h8*>(pa + kk * 32);
@@ -1352,8 +1368,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int t = 0; t < TPC; ++t) {
         const int o1 = (kk * 16 + trk) * SF + (t * 32 + trc) * 2;
         const h8 bh = tr_pair(buf + o1, 4 * SF);
-        const h8 bl = tr_pair(buf + FPLANE + o1, 4 * SF);
-        acc[t] = mfma_x3(ah, al, bh, bl, acc[t]);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[t], 0, 0, 0);
+        if (!zlo) {
+          const h8 bl = tr_pair(buf + FPLANE + o1, 4 * SF);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[t], 0, 0, 0);
+        }
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[t], 0, 0, 0);
       }
     }
     if (++cs == nst) {  // chunk done: store its tile, restart the accumulators
@@ -2335,7 +2355,7 @@ float split_scale(float max_abs) {
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
-         hipStream_t st, int t0 = 0, float x3_max = 0.0f, bool pre = false) {
+         hipStream_t st, int t0 = 0, float x3_max = 0.0f, bool pre = false, int lzs = 0) {
   const GramPlan g = gram_plan(N, K, symmetric != 0, t0);
   if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
@@ -2416,7 +2436,7 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
       auto go3 = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds, st, X,
                            N, (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks, sc,
-                           part);
+                           part, lzs);
       };
       if (pre) go3(gram_kernel3<true>);
       else go3(gram_kernel3<false>);
@@ -3027,6 +3047,29 @@ extern "C" int trex_tree_gram_skip_x3p(const void* S16, int N, int64_t K, int sk
   const float* S = static_cast<const float*>(S16);
   return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream,
               skip_rows / 64, max_abs, true);
+}
+
+// the same Gram with the leaf rows declared exact one-hot by their codes
+// (the buffer trex_tree_leaf_codes filled with status 0): their f16 lo plane
+// is zero, so the lo x hi products of the leaf strips are skipped (bitwise
+// the plain call; the codes themselves are not read)
+extern "C" int trex_tree_gram_skip_x3p_codes(const void* S16, int N, int64_t K, int skip_rows,
+                                             float max_abs, const void* codes, int64_t codes_bytes,
+                                             int n_leaf, int Q, float* G, void* workspace,
+                                             int64_t workspace_bytes, void* stream) {
+  if (!S16 || !G || !workspace || N <= 0 || K <= 0 || K > 0x7FFFFFFF || skip_rows < 0 ||
+      skip_rows > N || !pos_finite_f32(max_abs) || K % 4 != 0)
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3p_codes: bad arguments");
+  const int lcr = trex_tree_leaf_code_rows(n_leaf);
+  if (!codes || Q != 4 || lcr <= 0 || lcr > N || codes_bytes < (int64_t)lcr * (K / Q))
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3p_codes: bad codes (Q = 4, n_leaf >= 32)");
+  if (workspace_bytes < trex_tree_workspace_bytes(N, K))
+    return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3p_codes: workspace too small");
+  const float* S = static_cast<const float*>(S16);
+  const char* ev = std::getenv("TREX_GRAM_LZ");  // A/B: 0 = every product computed
+  const int lzs = (ev && std::atoi(ev) == 0) ? 0 : lcr / 32;
+  return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream,
+              skip_rows / 64, max_abs, true, lzs);
 }
 
 extern "C" int trex_tree_mf_rows_x3p(const void* M16, int ldm, const void* S16, int N, int64_t K,

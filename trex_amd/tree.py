@@ -557,7 +557,12 @@ class TreeOptimizer:
 
     def _gram(self, st):
         N, K = self.N, self.K
-        if self.presplit:
+        if self.presplit and self.codes is not None:
+            # exact one-hot leaf rows: their zero lo plane's products skipped
+            check(lib().trex_tree_gram_skip_x3p_codes(
+                ptr(self.S16), N, K, self.skip_rows, 1.0, ptr(self.codes), self.codes.numel(),
+                self.n_leaf, self.Q, ptr(self.G), ptr(self.ws), self.ws.numel(), st))
+        elif self.presplit:
             check(lib().trex_tree_gram_skip_x3p(ptr(self.S16), N, K, self.skip_rows, 1.0,
                                                 ptr(self.G), ptr(self.ws), self.ws.numel(), st))
         elif self.gemm == "x3":
