@@ -317,6 +317,22 @@ __device__ __forceinline__ void bld_row(rsrc_t r, int voff, int soff, float (&d)
   }
 }
 
+#ifdef TREX_DIAG_PAD
+// sensitivity probe (diagnostic builds only, wrong timing on purpose, same
+// results): TREX_DIAG_SALU / TREX_DIAG_VALU independent dummy scalar /
+// vector adds per tree step, to see which issue stream the time follows
+__device__ __forceinline__ void diag_pad(float& v) {
+  int sd = 0;
+#pragma unroll
+  for (int i = 0; i < TREX_DIAG_SALU; ++i) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sd));
+  float t = 0.0f;
+#pragma unroll
+  for (int i = 0; i < TREX_DIAG_VALU; ++i) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(t));
+  asm volatile("" ::"s"(sd), "v"(t));
+  (void)v;
+}
+#endif
+
 // s_i = sum_j K_ij u_j for every parent state i.  SYM (K = K^T, symmetric
 // C): s_i = sum_j K_ji u_j, accumulated over j with the row pairs (K_j,2p,
 // K_j,2p+1) already in SGPRs -- Q / 2 v_pk_fma_f32 per j (8 at Q = 4) instead
@@ -817,7 +833,14 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         }
         const int row = stp.x & 0xFFFF;
         const int oslot = (stp.x >> 16) & 0xFF;
+#ifdef TREX_DIAG_PAD
+        diag_pad(dv[0][0]);
+#endif
+#ifdef TREX_DIAG_NOSTORE
+        bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, 0x7FFFFFF0, row * rowbytes, dv);
+#else
         bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, voff, row * rowbytes, dv);
+#endif
         if (!(stp.w & kStepToNext) && oslot != 0xFF) {
           lds_put<Q, SPT>(slots, oslot, lane, dv);
         }
@@ -878,7 +901,11 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           // deferred cherries (kChildDeferred) are recomputed, not re-read
           const bool internal =
               ((desc >> 24) & 3) == kKindInt && !(desc & kChildDeferred);
+#ifdef TREX_DIAG_NOLOAD
+          const int vo = 0x7FFFFFF0 + 0 * (internal ? voff : 0);
+#else
           const int vo = internal ? voff : 0x7FFFFFF0;
+#endif
           const int crow = internal ? (desc & 0xFFFF) : 0;
           bld_row<Q, SPT, FWD ? kAuxFusedRow : kAuxAdjRow>(rdp, vo, crow * rowbytes, nd[c]);
         }
@@ -887,6 +914,9 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
       auto bstep = [&](const I4& stp, float (&cd)[2][Q][SPT]) {
         if (stp.w & kStepUnreached) return;
         const int row = stp.x & 0xFFFF;
+#ifdef TREX_DIAG_PAD
+        diag_pad(acc[0][0]);
+#endif
         float g[Q][SPT];
         if (stp.w & kStepToNext) {
 #pragma unroll
