@@ -838,6 +838,11 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #endif
 #ifdef TREX_DIAG_NOSTORE
         bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, 0x7FFFFFF0, row * rowbytes, dv);
+#elif defined(TREX_DIAG_DROP)
+        // probe: the first (DROP > 0) or last (DROP < 0) |DROP| steps' stores dropped
+        const bool drop = TREX_DIAG_DROP > 0 ? k < TREX_DIAG_DROP : k >= n_int + TREX_DIAG_DROP;
+        bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, drop ? 0x7FFFFFF0 : voff,
+                                                        row * rowbytes, dv);
 #else
         bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, voff, row * rowbytes, dv);
 #endif
