@@ -824,7 +824,10 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
 #pragma unroll
               for (int s = 0; s < SPT; ++s) m[i][s] = d[c][i][s];
           } else {
-            message<Q, SPT, MODE, SYM>(cf, a, bcoef, d[c], m);
+            // the forward keeps the pair-wise dots in every kernel: the DP
+            // table is bitwise the same from the fused, forward-only and
+            // ragged launches (the symmetric-K form sums in another order)
+            message<Q, SPT, MODE, false>(cf, a, bcoef, d[c], m);
           }
 #pragma unroll
           for (int i = 0; i < Q; ++i)
