@@ -371,6 +371,57 @@ def test_fused_fwd_bwd_equals_separate_launches(device, tau, B, L):
         np.testing.assert_allclose(f.tree_score.cpu().numpy(), ref["tree_score"], rtol=SOFT_RTOL)
 
 
+def _pectinate(B, nl):
+    """caterpillar trees: node nl + i joins leaf i + 1 to node nl + i - 1
+    (node nl the cherry (0, 1))."""
+    ch = -np.ones((B, 2 * nl - 1, 2), dtype=np.int32)
+    ch[:, nl] = (0, 1)
+    for i in range(1, nl - 1):
+        ch[:, nl + i] = (i + 1, nl + i - 1)
+    return ch
+
+
+@pytest.mark.parametrize("tau", [0.0, 0.5])
+@pytest.mark.parametrize("topo", ["random", "balanced", "pectinate"])
+def test_deferral_levels_agree(device, monkeypatch, tau, topo):
+    """Deferred cherry edges (plan.cpp, TREX_DEFER = 0 none / default on):
+    the adjoint rebuilds a deferred cherry's D exactly as the forward built
+    it, so the DP table, scores, marginals and ancestral states are bitwise
+    the undeferred run's; only the dC accumulation order moves (same value
+    within rounding; hard costs also vs fp64 -- with missing leaves the soft
+    dC carries the f32 1e5-sentinel rounding the other tests bound, the same
+    either way).  16 trees x 2 000 sites: the re-reading fused kernel of the
+    benchmark; caterpillar trees have one cherry each."""
+    B, L, Q = 16, 2000, 4
+    if topo == "random":
+        ch = random_topologies(B, 32, seed=41)
+    elif topo == "balanced":
+        ch = balanced_children(32, B=B)
+    else:
+        ch = _pectinate(B, 32)
+    leaves = random_leaves(B, 32, L, Q, seed=42, missing=0.02)
+    cost = int_cost(Q, seed=43, hi=4)
+    lv = _dev(leaves, device)
+    c = _dev(cost, device, torch.float32)
+    dts = torch.linspace(0.5, 2.0, B, device=device)
+    runs = []
+    for level in ("0", "1"):
+        monkeypatch.setenv("TREX_DEFER", level)
+        eng = _engine(ch, L, Q, device)
+        runs.append(eng.fwd_bwd(lv, c, tau, dts, site_score=True, marginals=True,
+                                anc_states=True))
+    ref = batched_fwd_bwd_ref(ch, leaves, cost, tau, d_tree_score=dts.cpu().numpy()) if tau == 0.0 else None
+    f0, dc0, mg0, an0 = runs[0]
+    for f, dc, mg, an in runs[1:]:
+        assert torch.equal(f.dp, f0.dp)
+        assert torch.equal(f.tree_score, f0.tree_score)
+        assert torch.equal(f.site_score, f0.site_score)
+        assert torch.equal(mg, mg0) and torch.equal(an, an0)
+        np.testing.assert_allclose(dc.cpu().numpy(), dc0.cpu().numpy(), rtol=1e-5, atol=1e-3)
+        if tau == 0.0:
+            np.testing.assert_allclose(dc.cpu().numpy(), ref["d_cost"], rtol=1e-6)
+
+
 def test_repeated_launches_reset_reduction_counters(device):
     """The in-kernel reductions leave their arrival counters at zero, so
     back-to-back launches (and hipGraph replays) keep producing the same sums."""
