@@ -451,14 +451,23 @@ def c5_gemm_kernels(torch, opt):
     # MF operand bytes: the code rows as one byte per site (leaf codes) or f32 rows
     lcr = int(L_.trex_tree_leaf_code_rows(nl)) if opt.codes is not None else 0
     s_mf = (N - lcr) * K * 4 + lcr * (K // opt.Q)
-    for name, fn, abytes, flops in (
-            ("gram", gram, N * K * 4 + N * N * 4, tiles * 32 * 32 * K * 2),
-            ("mf", mf, s_mf + N * N * 4 + na * K * 4, ((na + 31) // 32 * 32) * nt * 32 * K * 2)):
+    # f16x3 products issued per 32x32 tile-step: 3 (hi*hi + hi*lo + lo*hi),
+    # 2 where one operand is an exact one-hot leaf row (zero lo plane: the
+    # Gram's leaf strips when the codes declare them, the MF's code stages)
+    lzs = lcr // 32
+    g_leaf = (sum(nt - max(a, sk) for a in range(min(lzs, nt)))
+              if (opt.codes is not None and getattr(opt, "presplit", False)) else 0)
+    g_prod = (2 * g_leaf + 3 * (tiles - g_leaf)) / tiles if tiles else 3
+    m_prod = (2 * lzs + 3 * (nt - lzs)) / nt
+    for name, fn, abytes, flops, prod in (
+            ("gram", gram, N * K * 4 + N * N * 4, tiles * 32 * 32 * K * 2, g_prod),
+            ("mf", mf, s_mf + N * N * 4 + na * K * 4, ((na + 31) // 32 * 32) * nt * 32 * K * 2,
+             m_prod)):
         sec = timed(fn)
         d = {"us": round(sec * 1e6, 2), "algorithmic_bytes": abytes,
              "GBs": round(abytes / sec / 1e9, 1), "hbm_frac": round(abytes / sec / 1e9 / HBM_PEAK_GBS, 4)}
         if opt.gemm == "x3":
-            issued = 3 * flops  # hi*hi + hi*lo + lo*hi on f16 MFMA
+            issued = int(round(prod * flops))  # f16 MFMA flops actually issued
             d.update(mfma_flops_issued=issued,
                      mfma_tflops=round(issued / sec / 1e12, 1),
                      mfma_frac=round(issued / sec / 1e12 / MFMA_F16_DENSE_TFS, 4),
