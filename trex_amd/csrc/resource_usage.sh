@@ -1,7 +1,7 @@
 #!/bin/bash
 # Print per-kernel VGPR/SGPR/scratch/occupancy of libtrexhip's device code.
 cd "$(dirname "$0")"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-honor-nans -c --cuda-device-only \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-honor-nans $RU_FLAGS -c --cuda-device-only \
   -Rpass-analysis=kernel-resource-usage "${1:-sankoff.hip}" -o /tmp/_ru.o 2>&1 |
   grep -E 'Function Name|VGPRs:|TotalSGPRs|ScratchSize|Occupancy|Spill' |
   sed 's/ \[-Rpass-analysis=kernel-resource-usage\]//; s/^[^ ]* //; s/remark: //' |
