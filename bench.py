@@ -459,8 +459,11 @@ def c5_gemm_kernels(torch, opt):
               if (opt.codes is not None and getattr(opt, "presplit", False)) else 0)
     g_prod = (2 * g_leaf + 3 * (tiles - g_leaf)) / tiles if tiles else 3
     m_prod = (2 * lzs + 3 * (nt - lzs)) / nt
+    # the Gram reads whole 128-row passes of code rows as bytes (pre-split path)
+    gcr = (lcr // 128) * 128 if getattr(opt, "presplit", False) else 0
+    s_gram = (N - gcr) * K * 4 + gcr * (K // opt.Q)
     for name, fn, abytes, flops, prod in (
-            ("gram", gram, N * K * 4 + N * N * 4, tiles * 32 * 32 * K * 2, g_prod),
+            ("gram", gram, s_gram + N * N * 4, tiles * 32 * 32 * K * 2, g_prod),
             ("mf", mf, s_mf + N * N * 4 + na * K * 4, ((na + 31) // 32 * 32) * nt * 32 * K * 2,
              m_prod)):
         sec = timed(fn)

@@ -452,6 +452,7 @@ constexpr int kG3Rows = 512;
 constexpr int kG3Stride = 80;
 constexpr int kG3Tiles = 13;
 constexpr int kG3Waves = 8;
+constexpr int kG3Rows4 = kG3Waves * 64 / 4;  // rows per load pass (128)
 constexpr int kG3Buf = kG3Rows * kG3Stride;
 constexpr int kG3Lds = 2 * kG3Buf;
 
@@ -502,10 +503,17 @@ __device__ __forceinline__ void g3_stage(unsigned char* buf, int row, int sub, c
   *reinterpret_cast<h4*>(buf + row * kG3Stride + 32 + sub * 8) = lo;
 }
 
-template <bool PRE = false>  // PRE: S pre-split (split_x3_group layout)
+// NCP (PRE only): rows [0, 128 NCP) -- the first NCP row passes -- are exact
+// one-hot leaf rows read as their code bytes (codes, trex_tree_leaf_codes;
+// one byte per site instead of a 16-B pre-split piece) and expanded into
+// the same f16 image (hi = one-hot x sc, lo = 0): bitwise the pre-split rows.
+// The pass split is compile-time: a runtime per-row choice spilled (11-16
+// VGPRs) and cost the whole kernel 1.7x
+template <bool PRE = false, int NCP = 0>  // PRE: S pre-split (split_x3_group layout)
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void gram_kernel3(
     const float* __restrict__ S, int N, int K, int ns, int t0s, int ntiles, int ngroups,
-    int ksplit, int nchunks, float sc, float* __restrict__ part, int lzs = 0) {
+    int ksplit, int nchunks, float sc, float* __restrict__ part, int lzs = 0,
+    const uint8_t* __restrict__ codes = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds3[];
   const int g = blockIdx.x % ngroups;
   const int split = blockIdx.x / ngroups;
@@ -532,13 +540,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const rsrc_t rs = make_rsrc(S, (uint32_t)((size_t)N * K * 4));
   const int sub = tid & 3, rb = tid >> 2;
   constexpr int kRowsPerPass = kG3Waves * kWave / 4;
-  u32x4 pf[kG3Rows / kRowsPerPass];
+  static_assert(NCP == 0 || PRE, "code rows need the pre-split image");
+  u32x4 pf[kG3Rows / kRowsPerPass - NCP];
+  uint32_t pcode[NCP > 0 ? NCP : 1];
+  const rsrc_t rcd = make_rsrc(codes, (uint32_t)((size_t)kRowsPerPass * NCP * (K / 4)));
   auto gload = [&](int c) {
 #pragma unroll
-    for (int i = 0; i < kG3Rows / kRowsPerPass; ++i)
-      pf[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((rb + kRowsPerPass * i) * K + 4 * sub) * 4,
-                                                    c * 64, 0);
+    for (int i = 0; i < kG3Rows / kRowsPerPass; ++i) {
+      const int vo = ((rb + kRowsPerPass * i) * K + 4 * sub) * 4;  // code byte: vo / 16
+      if (i < NCP)
+        pcode[i < NCP ? i : 0] = __builtin_amdgcn_raw_buffer_load_b8(rcd, vo >> 4, c * 4, 0);
+      else
+        pf[i - NCP] = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, c * 64, 0);
+    }
   };
+  const uint32_t hb = (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)sc);  // one-hot 1 x sc
   // K % 16 != 0 (K % 4 == 0): the last chunk's columns past K hold the next
   // row's first values (or read out of bounds: 0); staged as zeros, they add
   // nothing to any product
@@ -546,7 +562,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const bool kv = 16 * c + 4 * sub < K;
 #pragma unroll
     for (int i = 0; i < kG3Rows / kRowsPerPass; ++i)
-      g3_stage<PRE>(buf, rb + kRowsPerPass * i, sub, kv ? pf[i] : (u32x4){0u, 0u, 0u, 0u}, sc);
+    {
+      const int row = rb + kRowsPerPass * i;
+      if (i < NCP) {
+        const uint32_t code = kv ? (pcode[i < NCP ? i : 0] & 0xFFu) : 0xFFu;
+        const u32x4 w = {(code == 0 ? hb : 0u) | ((code == 1 ? hb : 0u) << 16),
+                         (code == 2 ? hb : 0u) | ((code == 3 ? hb : 0u) << 16), 0u, 0u};
+        g3_stage<true>(buf, row, sub, w, sc);
+      } else {
+        g3_stage<PRE>(buf, row, sub, kv ? pf[i - NCP] : (u32x4){0u, 0u, 0u, 0u}, sc);
+      }
+    }
   };
   const int lofs = r * kG3Stride + 16 * h;
   auto compute = [&](const unsigned char* buf) {
@@ -2355,7 +2381,8 @@ float split_scale(float max_abs) {
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 // x3_max > 0: f16x3 split products with operands bounded by x3_max
 int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float* G, float* part,
-         hipStream_t st, int t0 = 0, float x3_max = 0.0f, bool pre = false, int lzs = 0) {
+         hipStream_t st, int t0 = 0, float x3_max = 0.0f, bool pre = false, int lzs = 0,
+         const uint8_t* codes = nullptr) {
   const GramPlan g = gram_plan(N, K, symmetric != 0, t0);
   if (g.npairs == 0) return TREX_OK;
   const int ks8 = (g.ksplit + 7) / 8 * 8;
@@ -2375,6 +2402,10 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3<false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3<true, 1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gram_kernel3<true, 2>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, kG3Lds);
       return true;
     }();
@@ -2436,9 +2467,13 @@ int gram(const float* X, const float* Y, int N, int64_t K, int symmetric, float*
       auto go3 = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(p.ksplit * p.ngroups), dim3(kG3Waves * kWave), kG3Lds, st, X,
                            N, (int)K, p.ns, p.t0s, p.ntiles, p.ngroups, p.ksplit, p.nchunks, sc,
-                           part, lzs);
+                           part, lzs, codes);
       };
-      if (pre) go3(gram_kernel3<true>);
+      // code rows by compile-time passes of 128 rows (C5: 256 leaves, 2)
+      const int ncp = (pre && codes && lzs > 0 && (32 * lzs) % kG3Rows4 == 0) ? 32 * lzs / kG3Rows4 : 0;
+      if (pre && ncp == 1) go3(gram_kernel3<true, 1>);
+      else if (pre && ncp == 2) go3(gram_kernel3<true, 2>);
+      else if (pre) go3(gram_kernel3<true>);
       else go3(gram_kernel3<false>);
     }
     hipLaunchKernelGGL(gram3_reduce_kernel, dim3(p.ntiles * 16), dim3(256), 0, st, part, N, p.ns,
@@ -3051,8 +3086,9 @@ extern "C" int trex_tree_gram_skip_x3p(const void* S16, int N, int64_t K, int sk
 
 // the same Gram with the leaf rows declared exact one-hot by their codes
 // (the buffer trex_tree_leaf_codes filled with status 0): their f16 lo plane
-// is zero, so the lo x hi products of the leaf strips are skipped (bitwise
-// the plain call; the codes themselves are not read)
+// is zero, so the lo x hi products of the leaf strips are skipped, and the
+// code rows are read as their bytes instead of 16-B pre-split pieces
+// (bitwise the plain call)
 extern "C" int trex_tree_gram_skip_x3p_codes(const void* S16, int N, int64_t K, int skip_rows,
                                              float max_abs, const void* codes, int64_t codes_bytes,
                                              int n_leaf, int Q, float* G, void* workspace,
@@ -3066,10 +3102,15 @@ extern "C" int trex_tree_gram_skip_x3p_codes(const void* S16, int N, int64_t K, 
   if (workspace_bytes < trex_tree_workspace_bytes(N, K))
     return set_error(TREX_E_ARG, "trex_tree_gram_skip_x3p_codes: workspace too small");
   const float* S = static_cast<const float*>(S16);
-  const char* ev = std::getenv("TREX_GRAM_LZ");  // A/B: 0 = every product computed
-  const int lzs = (ev && std::atoi(ev) == 0) ? 0 : lcr / 32;
+  // TREX_GRAM_LZ (A/B): 0 = every product computed, rows as pre-split f16;
+  // 1 = zero-plane products skipped, rows pre-split; default: also the code
+  // rows read as their bytes
+  const char* ev = std::getenv("TREX_GRAM_LZ");
+  const int lz = ev ? std::atoi(ev) : 2;
+  const int lzs = lz == 0 ? 0 : lcr / 32;
   return gram(S, S, N, K, 1, G, static_cast<float*>(workspace), (hipStream_t)stream,
-              skip_rows / 64, max_abs, true, lzs);
+              skip_rows / 64, max_abs, true, lzs,
+              lz >= 2 ? static_cast<const uint8_t*>(codes) : nullptr);
 }
 
 extern "C" int trex_tree_mf_rows_x3p(const void* M16, int ldm, const void* S16, int N, int64_t K,
