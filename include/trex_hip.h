@@ -374,8 +374,11 @@ int trex_tree_gram_skip_x3p(const void* S16, int N, int64_t K, int skip_rows, fl
 /* trex_tree_gram_skip_x3p_codes: the same Gram with rows [0, 32 (n_leaf / 32))
  * declared exact one-hot by their codes (the buffer trex_tree_leaf_codes
  * filled, status 0; Q = 4): their f16 lo plane is zero, so the lo x hi
- * products of those strips are skipped -- bitwise trex_tree_gram_skip_x3p.
- * tree.py:199-209 (the surrogate's S S^T).  Round 6. */
+ * products of those strips are skipped, and whole 128-row passes of them
+ * are read as their code bytes instead of S16's 16-B pieces -- bitwise
+ * trex_tree_gram_skip_x3p (S16's code rows must hold exactly the split of
+ * the one-hot rows at this max_abs).  tree.py:199-209 (the surrogate's
+ * S S^T).  Round 6. */
 int trex_tree_gram_skip_x3p_codes(const void* S16, int N, int64_t K, int skip_rows, float max_abs,
                                   const void* codes, int64_t codes_bytes, int n_leaf, int Q,
                                   float* G, void* workspace, int64_t workspace_bytes,
