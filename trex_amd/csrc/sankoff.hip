@@ -274,7 +274,12 @@ __device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT
 // and marginal stores stream (C4 forward 620 -> 560 us, adjoint 588 -> ~577
 // us); the fused kernel re-reads its rows within the same wave's life, from
 // L2 / MALL in part, so its accesses stay temporal
+#ifndef TREX_CHERRY_NT
+#define TREX_CHERRY_NT 2
+#endif
 constexpr int kAuxFwdRow = TREX_AUX_FWD, kAuxFusedRow = TREX_AUX_FUSED;
+// the fused kernel's stores of deferred-cherry rows (never re-read)
+constexpr int kAuxCherryRow = TREX_CHERRY_NT ? TREX_CHERRY_NT : TREX_AUX_FUSED;
 constexpr int kAuxAdjRow = TREX_AUX_ADJ, kAuxMarg = TREX_AUX_MARG;
 
 // AUX: the buffer instruction's cache-policy bits (2 = nt: a streaming
@@ -847,7 +852,14 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
         bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, drop ? 0x7FFFFFF0 : voff,
                                                         row * rowbytes, dv);
 #else
-        bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, voff, row * rowbytes, dv);
+        // rows the adjoint never re-reads (deferred cherries) stream past the
+        // caches (nt), so the re-read rows keep more of L2 / MALL: the
+        // 128-tree shard 134 -> 128 us, the full batch unchanged (its table
+        // is ~10x the MALL); TREX_CHERRY_NT=0 builds the uniform policy
+        if (BWD && kAuxCherryRow != kAuxFusedRow && (stp.w & kStepDeferredIn))
+          bst_row<Q, SPT, kAuxCherryRow>(rdp, voff, row * rowbytes, dv);
+        else
+          bst_row<Q, SPT, BWD ? kAuxFusedRow : kAuxFwdRow>(rdp, voff, row * rowbytes, dv);
 #endif
         if (!(stp.w & kStepToNext) && oslot != 0xFF) {
           lds_put<Q, SPT>(slots, oslot, lane, dv);
