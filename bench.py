@@ -727,15 +727,6 @@ def main():
     step = Step(torch, eng, leaves, cost, tau)
     red = torch.zeros(Q * Q + 1, dtype=torch.float32, device=device)
 
-    use_graph = not args.no_graph
-    graph = None
-    step()
-    torch.cuda.synchronize()
-    if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
-
     # N > 1: the step's [dC, loss] all-reduce runs on a side stream and
     # overlaps the next step's kernel (double-buffered, as DDP overlaps its
     # gradient buckets with backward); every all-reduce completes inside the
@@ -748,19 +739,43 @@ def main():
     ar_events = []
     ar_timing = [False]
 
+    def fill(buf):
+        # the all-reduce payload [dC, loss], written inside the step's graph
+        # (eager, these were three extra launches of ~4 us each per step)
+        buf[:Q * Q].copy_(step.out_b["d_cost"].view(-1))
+        torch.sum(step.out_f["tree_score"], dim=0, keepdim=True, out=buf[Q * Q:])
+
+    use_graph = not args.no_graph
+    graphs = None  # [buffer 0, buffer 1] step graphs (one without dist)
+    step()
+    if dist_on:
+        fill(reds[0])
+    torch.cuda.synchronize()
+    if use_graph:
+        graphs = []
+        for i in range(2 if dist_on else 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+                if dist_on:
+                    fill(reds[i])
+            graphs.append(g)
+
     def run_once():
-        if graph is not None:
-            graph.replay()
+        i = it[0] % 2
+        if dist_on:
+            it[0] += 1
+            # the all-reduce two steps back has read this buffer
+            torch.cuda.current_stream(device).wait_event(done[i])
+        if graphs is not None:
+            graphs[i if dist_on else 0].replay()
         else:
             step()
+            if dist_on:
+                fill(reds[i])
         if dist_on:
-            i = it[0] % 2
-            it[0] += 1
             buf = reds[i]
             cur = torch.cuda.current_stream(device)
-            cur.wait_event(done[i])  # the all-reduce two steps back has read buf
-            buf[:Q * Q].copy_(step.out_b["d_cost"].view(-1))
-            buf[Q * Q:].copy_(step.out_f["tree_score"].sum().view(1))
             comm.wait_stream(cur)
             with torch.cuda.stream(comm):
                 if ar_timing[0]:
