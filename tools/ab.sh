@@ -19,7 +19,7 @@ for rep in $(seq ${REPS:-2}); do
 import json,sys
 d=json.load(open(sys.argv[1]))
 x = ''
-if 'c4_shard' in d: x += ' shard %.1f us' % d['c4_shard']['fused_kernel_us']
+if 'c4_shard' in d: x += ' shard %.1f us (step %.1f us)' % (d['c4_shard']['fused_kernel_us'], d['c4_shard']['ms_per_step'] * 1e3)
 if 'c2' in d: x += ' c2 %.1f us' % (d['c2']['ms_per_step']*1e3)
 if 'c3' in d: x += ' c3 soft %.1f hard %.1f us' % (d['c3']['soft_ms_per_step']*1e3, d['c3']['hard_recon_ms_per_step']*1e3)
 if 'c5' in d:
