@@ -278,6 +278,13 @@ __device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT
 #define TREX_CHERRY_NT 2
 #endif
 constexpr int kAuxFwdRow = TREX_AUX_FWD, kAuxFusedRow = TREX_AUX_FUSED;
+#ifndef TREX_AUX_FUSED_LOAD
+#define TREX_AUX_FUSED_LOAD 2
+#endif
+// the fused kernel's adjoint re-reads of its own rows: nt (each row is read
+// once, then dead; with the never-re-read cherry rows also streamed, fused
+// 929-934 -> 903-911 us same box, PERFLOG; the stores stay temporal)
+constexpr int kAuxFusedLoad = TREX_AUX_FUSED_LOAD;
 // the fused kernel's stores of deferred-cherry rows (never re-read)
 constexpr int kAuxCherryRow = TREX_CHERRY_NT ? TREX_CHERRY_NT : TREX_AUX_FUSED;
 constexpr int kAuxAdjRow = TREX_AUX_ADJ, kAuxMarg = TREX_AUX_MARG;
@@ -927,7 +934,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
           const int vo = internal ? voff : 0x7FFFFFF0;
 #endif
           const int crow = internal ? (desc & 0xFFFF) : 0;
-          bld_row<Q, SPT, FWD ? kAuxFusedRow : kAuxAdjRow>(rdp, vo, crow * rowbytes, nd[c]);
+          bld_row<Q, SPT, FWD ? kAuxFusedLoad : kAuxAdjRow>(rdp, vo, crow * rowbytes, nd[c]);
         }
       };
       float gnext[Q][SPT];  // cotangent handed to the next reverse step (bypass)
