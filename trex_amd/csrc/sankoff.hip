@@ -274,6 +274,9 @@ __device__ __forceinline__ void bld(rsrc_t r, int voff, int soff, float (&o)[SPT
 // and marginal stores stream (C4 forward 620 -> 560 us, adjoint 588 -> ~577
 // us); the fused kernel re-reads its rows within the same wave's life, from
 // L2 / MALL in part, so its accesses stay temporal
+#ifndef TREX_AUX_LEAF
+#define TREX_AUX_LEAF 0  // the leaf-tile prefetch loads
+#endif
 #ifndef TREX_CHERRY_NT
 #define TREX_CHERRY_NT 2
 #endif
@@ -714,7 +717,7 @@ __device__ __forceinline__ void sankoff_body(const KArgs& A, float* lds) {
     const rsrc_t rl = make_rsrc(A.leaves + (size_t)tr * A.nl * L, (uint32_t)((size_t)A.nl * L));
 #pragma unroll
     for (int r = 0; r < kPrefetchRows / 4; ++r)
-      pre[r] = __builtin_amdgcn_raw_buffer_load_b32(rl, pf_voff, 4 * r * L + tl * kWave, 0);
+      pre[r] = __builtin_amdgcn_raw_buffer_load_b32(rl, pf_voff, 4 * r * L + tl * kWave, TREX_AUX_LEAF);
   };
   auto store_prefetch = [&]() {
     uint32_t* dst = reinterpret_cast<uint32_t*>(lleaf);
