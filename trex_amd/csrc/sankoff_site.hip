@@ -44,7 +44,11 @@
 
 namespace trex {
 
+#ifndef TREX_SITE_LOAD_AUX
+#define TREX_SITE_LOAD_AUX 1  // cache policy of the adjoint's DP-row re-reads (1 = sc0)
+#endif
 namespace {
+constexpr int kSiteLoadAux = TREX_SITE_LOAD_AUX;
 
 constexpr int kSQ = kSiteSQ;               // states per lane (Q padded to 20)
 constexpr int kSWv = 8;                    // waves per workgroup
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
 #pragma unroll
       for (int c = 0; c < kSQ / 4; ++c) {
         u32x4 w = u32x4{0, 0, 0, 0};
-        if (4 * c < Q) w = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 16 * c, row * rowbytes, 1);
+        if (4 * c < Q) w = __builtin_amdgcn_raw_buffer_load_b128(rr, vbase + 16 * c, row * rowbytes, kSiteLoadAux);
         v[4 * c] = __uint_as_float(w.x);
         v[4 * c + 1] = __uint_as_float(w.y);
         v[4 * c + 2] = __uint_as_float(w.z);
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
     } else {
 #pragma unroll
       for (int j = 0; j < kSQ; ++j)
-        v[j] = j < Q ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, vbase + 4 * j, row * rowbytes, 1))
+        v[j] = j < Q ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, vbase + 4 * j, row * rowbytes, kSiteLoadAux))
                      : 0.0f;
     }
   };
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         if (4 * c < Q) {
           const int o = 16 * (lane + kWave * c);
           const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rr, o < tbytes ? tb + o : 0x7FFFFFF0,
-                                                               row * rowbytes, 1);
+                                                               row * rowbytes, kSiteLoadAux);
           *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(xr) + o) = w;
         }
       }
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(kSWv * kWave, 1) void sankoff_site_kernel(SiteArgs 
         if (j < Q) {
           const int o = 4 * (lane + kWave * j);
           xr[lane + kWave * j] = __uint_as_float(
-              __builtin_amdgcn_raw_buffer_load_b32(rr, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, 1));
+              __builtin_amdgcn_raw_buffer_load_b32(rr, o < tbytes ? tb + o : 0x7FFFFFF0, row * rowbytes, kSiteLoadAux));
         }
       }
       lds_sync();
