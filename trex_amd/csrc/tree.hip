@@ -2163,8 +2163,14 @@ __global__ __launch_bounds__(kAdamBlock) void adam_seq_update4_x3p_kernel(
   __builtin_nontemporal_store((fv4){p4[0], p4[1], p4[2], p4[3]}, p + r);
   __builtin_nontemporal_store((fv4){m4[0], m4[1], m4[2], m4[3]}, mu + r);
   __builtin_nontemporal_store((fv4){v4[0], v4[1], v4[2], v4[3]}, nu + r);
+#ifndef TREX_S16_NT
+  // the next S rows (pre-split) stay cacheable: the next step's Gram and MF
+  // read them (C5 x3 step 0.640-0.652 -> 0.624-0.628 ms same box, PERFLOG)
+  s_out[r] = __builtin_bit_cast(fv4, split_x3_group(s4[0], s4[1], s4[2], s4[3], sx));
+#else
   __builtin_nontemporal_store(__builtin_bit_cast(fv4, split_x3_group(s4[0], s4[1], s4[2], s4[3], sx)),
                               s_out + r);
+#endif
 }
 
 void launch_adam_seq(const float* ds, int64_t rows, int Q, float T, float Tn, float* p, float* mu,
